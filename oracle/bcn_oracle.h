@@ -1,0 +1,66 @@
+/*
+ * bcn_oracle.h -- CPU restatement of the reference BCn block search.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This library is the parity checker for the HIP
+ * product path in gfx_imagecompress_amd/.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it; the product never links it.
+ *
+ * Every function restates the algorithm of DeanoC/gfx_imagecompress (itself a
+ * remix of AMD Compressonator) for the default-quality path, citing the
+ * reference file:line it follows.  Parity pinning: see oracle/README.md and
+ * tests/test_oracle.py (SURVEY.md section 8(c) fingerprints of the compiled
+ * reference, recorded by the survey probe).
+ */
+#ifndef BCN_ORACLE_H_
+#define BCN_ORACLE_H_
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Image_CompressAMDBC1Block (amd_bcx_helpers.cpp:51-105).
+ * in: 16 texels RGBA float [0,1]; alpha_threshold01 <= 0 disables alpha.
+ * refinement_steps: AMD option RefinementSteps (default 1).  */
+void orc_bc1_block(const float in[64], int refinement_steps,
+                   float alpha_threshold01, uint8_t out[8]);
+
+/* Image_CompressAMDAlphaSingleModeBlock (amd_bcx_helpers.cpp:125-140). */
+void orc_bc4_block(const float in[16], uint8_t out[8]);
+
+/* BC7BlockEncoder::CompressBlock (amd_bc7_body.cpp:1289-1465) with the
+ * encoder constructed as in Image_CompressAMDMultiModeLDRBlock
+ * (amd_bc7_compressor.cpp:11-23).  Returns the encoder's block error. */
+double orc_bc7_block(const float in[64], uint8_t mode_mask, int src_has_alpha,
+                     float quality, int colour_restrict, int alpha_restrict,
+                     float performance, uint8_t out[16]);
+
+/* Image-level drivers over an 8-bit source (the reference's block loops in
+ * amd_bc{1,4,5,7}_compressor.cpp with ReadNxNBlockF edge clamping,
+ * block_utils.cpp:7-41, and UNORM8 -> float as v/255.0f).
+ * src: rows of width*channels bytes, slices stacked; dst: row-major blocks.
+ * fmt: 1 = BC1, 4 = BC4, 5 = BC5, 7 = BC7.  channels in {1,2,3,4}.
+ * bc4_channel selects the source channel for BC4 (reference uses 1).
+ * first_row/num_rows restrict to a block-row range (per slice); rows <0 = all.
+ * threads: 0/1 = calling thread, N = a pool of N pthreads over block rows. */
+int orc_encode_image(int fmt, const uint8_t *src, uint32_t width, uint32_t height,
+                     uint32_t slices, uint32_t channels, int bc4_channel,
+                     int32_t first_row, int32_t num_rows, int threads,
+                     uint8_t *dst, double *block_err);
+
+/* helpers exposed for unit tests */
+void orc_load_block_rgba8(const uint8_t *src, uint32_t width, uint32_t height,
+                          uint32_t channels, uint32_t bx, uint32_t by,
+                          int force_alpha_one, float out[64]);
+uint64_t orc_fnv1a64(const uint8_t *p, size_t n);
+/* BC7 reference-style ramp value used by the shakers (amd_shake.cpp:283-286) */
+int orc_bc7_shake_ramp(int clog, int bits, int p1, int p2, int i);
+/* decode one BC7 block to RGBA8 (for tolerance checks) */
+void orc_bc7_decode(const uint8_t blk[16], uint8_t rgba[64]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,1333 @@
+/*
+ * orc_bc7.c -- CPU restatement of the reference BC7 encoder (default path).
+ *
+ * TEST INFRASTRUCTURE ONLY (see bcn_oracle.h).  Restates
+ *   src/amd_bc7_body.cpp        (mode loop, single/dual index search, packing)
+ *   src/amd_bc7_3dquant_vpc.cpp (optQuantAnD_d and helpers)
+ *   src/amd_shake.cpp           (init_ramps tables, ep_shaker_d, ep_shaker_2_d,
+ *                                quant_single_point_d)
+ * of DeanoC/gfx_imagecompress.  All arithmetic is IEEE double in the
+ * reference's association order (build with -ffp-contract=off).  Sorts whose
+ * ties matter use a stable sort, matching glibc 2.35's merge-sort qsort.
+ *
+ * Not restated (outside the default path; rejected with a negative error):
+ * optQuantTrace_d (only reached when performance < 1, amd_bc7_body.cpp:606).
+ *
+ * Shaker ramps: amd_shake.cpp:236 tests USE_FINAL_BC7_WEIGHTS, which is only
+ * defined in amd_bc7_body.cpp:60, so that translation unit builds its ramp
+ * table from the pure linear weights k/(2^n-1) (amd_shake.cpp:244-251).
+ */
+#include "bcn_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <pthread.h>
+#include <string.h>
+
+#include "bc7_tables.h"
+
+enum { PAR_CART = 0, PAR_SAME = 1, PAR_BCC = 2 };
+enum { ENC_NO_ALPHA = 0, ENC_COMBINED = 1, ENC_SEPARATE = 2 };
+
+/* bti[8], amd_bc7_body.cpp:84-94 */
+typedef struct {
+    int enc, part_bits, rot_bits, idxmode_bits, scalar_bits, vector_bits, pbit, subsets, ib0, ib1;
+} mode_info;
+static const mode_info kModes[8] = {
+    {ENC_NO_ALPHA, 4, 0, 0, 0, 12, 2, 3, 3, 0},
+    {ENC_NO_ALPHA, 6, 0, 0, 0, 18, 1, 2, 3, 0},
+    {ENC_NO_ALPHA, 6, 0, 0, 0, 15, 0, 3, 2, 0},
+    {ENC_NO_ALPHA, 6, 0, 0, 0, 21, 2, 2, 2, 0},
+    {ENC_SEPARATE, 0, 2, 1, 6, 15, 0, 1, 2, 3},
+    {ENC_SEPARATE, 0, 2, 0, 8, 21, 0, 1, 2, 2},
+    {ENC_COMBINED, 0, 0, 0, 0, 28, 2, 1, 4, 0},
+    {ENC_COMBINED, 6, 0, 0, 0, 20, 2, 2, 2, 0},
+};
+
+/* ------------------------------------------------------- shake tables --- */
+/* init_ramps, amd_shake.cpp:261-348.  ramp[] is evaluated on demand with the
+ * same double expression; sp_idx/sp_err are built once. */
+static double g_ep[4][256];
+static int g_sp_idx[3][4][256][2][2][16][2];
+static double g_sp_err[3][4][256][2][2][16];
+static pthread_once_t g_once = PTHREAD_ONCE_INIT;
+
+static const double kLinW[5][16] = {
+    {0.0},
+    {0.0, 1.0},
+    {0.0, 1.0 / 3.0, 2.0 / 3.0, 1.0},
+    {0.0, 1.0 / 7.0, 2.0 / 7.0, 3.0 / 7.0, 4.0 / 7.0, 5.0 / 7.0, 6.0 / 7.0, 1.0},
+    {0.0, 1.0 / 15.0, 2.0 / 15.0, 3.0 / 15.0, 4.0 / 15.0, 5.0 / 15.0, 6.0 / 15.0, 7.0 / 15.0,
+     8.0 / 15.0, 9.0 / 15.0, 10.0 / 15.0, 11.0 / 15.0, 12.0 / 15.0, 13.0 / 15.0, 14.0 / 15.0, 1.0}};
+
+static int expand_code(int bits, int v) { return (v << (8 - bits)) | (v >> (2 * bits - 8)); }
+
+static double shake_ramp(int clog, int bits, int p1, int p2, int i)
+{
+    const double *e = g_ep[bits - 5];
+    return floor(e[p1] + kLinW[clog][i] * (e[p2] - e[p1]) + 0.5);
+}
+
+static void build_tables(void)
+{
+    for (int bits = 5; bits < 9; ++bits)
+        for (int p = 0; p < (1 << bits); ++p)
+            g_ep[bits - 5][p] = (double)expand_code(bits, p);
+    for (int c = 0; c < 3; ++c)
+        for (int b = 0; b < 4; ++b)
+            for (int v = 0; v < 256; ++v)
+                for (int o1 = 0; o1 < 2; ++o1)
+                    for (int o2 = 0; o2 < 2; ++o2)
+                        for (int i = 0; i < 16; ++i) {
+                            g_sp_idx[c][b][v][o1][o2][i][0] = -1;
+                            g_sp_idx[c][b][v][o1][o2][i][1] = 0;
+                            g_sp_err[c][b][v][o1][o2][i] = DBL_MAX;
+                        }
+    for (int clog = 2; clog < 5; ++clog)
+        for (int bits = 5; bits < 9; ++bits)
+            for (int p1 = 0; p1 < (1 << bits); ++p1)
+                for (int p2 = 0; p2 < (1 << bits); ++p2)
+                    for (int i = 0; i < (1 << clog); ++i) {
+                        int v = (int)shake_ramp(clog, bits, p1, p2, i);
+                        g_sp_idx[clog - 2][bits - 5][v][p1 & 1][p2 & 1][i][0] = p1;
+                        g_sp_idx[clog - 2][bits - 5][v][p1 & 1][p2 & 1][i][1] = p2;
+                        g_sp_err[clog - 2][bits - 5][v][p1 & 1][p2 & 1][i] = 0.;
+                    }
+    for (int c = 0; c < 3; ++c)
+        for (int b = 0; b < 4; ++b)
+            for (int v = 0; v < 256; ++v)
+                for (int o1 = 0; o1 < 2; ++o1)
+                    for (int o2 = 0; o2 < 2; ++o2)
+                        for (int i = 0; i < (1 << (c + 2)); ++i) {
+                            if (g_sp_idx[c][b][v][o1][o2][i][0] >= 0) continue;
+                            int k;
+                            for (k = 1; k < 256; ++k)
+                                if ((v - k >= 0 && g_sp_err[c][b][v - k][o1][o2][i] == 0) ||
+                                    (v + k < 256 && g_sp_err[c][b][v + k][o1][o2][i] == 0))
+                                    break;
+                            if (v - k >= 0 && g_sp_err[c][b][v - k][o1][o2][i] == 0) {
+                                g_sp_idx[c][b][v][o1][o2][i][0] = g_sp_idx[c][b][v - k][o1][o2][i][0];
+                                g_sp_idx[c][b][v][o1][o2][i][1] = g_sp_idx[c][b][v - k][o1][o2][i][1];
+                            } else if (v + k < 256 && g_sp_err[c][b][v + k][o1][o2][i] == 0) {
+                                g_sp_idx[c][b][v][o1][o2][i][0] = g_sp_idx[c][b][v + k][o1][o2][i][0];
+                                g_sp_idx[c][b][v][o1][o2][i][1] = g_sp_idx[c][b][v + k][o1][o2][i][1];
+                            }
+                            g_sp_err[c][b][v][o1][o2][i] = (double)(k * k);
+                        }
+}
+
+int orc_bc7_shake_ramp(int clog, int bits, int p1, int p2, int i)
+{
+    pthread_once(&g_once, build_tables);
+    return (int)shake_ramp(clog, bits, p1, p2, i);
+}
+
+/* npv_nd / par_vectors_nd, amd_shake.cpp:42-217: only the types the BC7
+ * modes reach (CART, SAME_PAR, BCC) for 3 and 4 channels. */
+static const int kParCount[3] = {1, 2, 4};
+static const int kParVec[3][4][2] = {
+    /* CART */ {{0, 0}},
+    /* SAME */ {{0, 0}, {1, 1}},
+    /* BCC  */ {{0, 0}, {0, 1}, {1, 0}, {1, 1}},
+};
+
+static int clog_of(int last) { int c = 0, i = last + 1; while (i >>= 1) c++; return c; }
+
+/* ep_find_floor, amd_shake.cpp:351-367 */
+static int ep_floor(double v, int bits, int use_par, int odd)
+{
+    const double *p = g_ep[bits - 5];
+    int i1 = 0, i2 = 1 << (bits - use_par);
+    odd = use_par ? odd : 0;
+    while (i2 - i1 > 1) {
+        int j = (i1 + i2) / 2;
+        if (v >= p[(j << use_par) + odd])
+            i1 = j;
+        else
+            i2 = j;
+    }
+    return (i1 << use_par) + odd;
+}
+
+/* ------------------------------------------------------ 3D quantiser --- */
+typedef struct { double d; int i; } keyed;
+
+/* stable ascending sort by d (glibc msort order for a_compare ties) */
+static void stable_sort(keyed *a, int n)
+{
+    for (int i = 1; i < n; ++i) {
+        keyed t = a[i];
+        int j = i - 1;
+        while (j >= 0 && a[j].d - t.d > 0) {
+            a[j + 1] = a[j];
+            --j;
+        }
+        a[j + 1] = t;
+    }
+}
+
+/* sortProjection, amd_bc7_3dquant_vpc.cpp:138-150 */
+static void sort_order(const double *v, int *order, int n)
+{
+    keyed w[64];
+    for (int i = 0; i < n; ++i) {
+        w[i].i = i;
+        w[i].d = v[i];
+    }
+    stable_sort(w, n);
+    for (int i = 0; i < n; ++i) order[i] = w[i].i;
+}
+
+/* eigenVector_d, amd_bc7_3dquant_vpc.cpp:336-420 (p = 8, q = 3) */
+static void principal_vector(double cov[4][4], double vec[4], int dim)
+{
+    double c[2][4][4];
+    for (int i = 0; i < dim; ++i)
+        for (int j = 0; j < dim; ++j) c[0][i][j] = cov[i][j];
+    int l = 0;
+    for (int n = 0; n < 3; ++n) {
+        double md = 0;
+        for (int i = 0; i < dim; ++i) md = c[l][i][i] > md ? c[l][i][i] : md;
+        if (md <= 0) return;
+        for (int i = 0; i < dim; ++i)
+            for (int j = 0; j < dim; ++j) c[l][i][j] /= md;
+        for (int m = 0; m < 8; ++m) {
+            for (int i = 0; i < dim; ++i)
+                for (int j = 0; j < dim; ++j) {
+                    double t = 0;
+                    for (int k = 0; k < dim; ++k) t += c[l][i][k] * c[l][k][j];
+                    c[1 - l][i][j] = t;
+                }
+            l = 1 - l;
+        }
+    }
+    double md = 0;
+    int k = 0;
+    for (int i = 0; i < dim; ++i) {
+        k = c[l][i][i] > md ? i : k;
+        md = c[l][i][i] > md ? c[l][i][i] : md;
+    }
+    double t = 0;
+    for (int i = 0; i < dim; ++i) {
+        t += c[l][k][i] * c[l][k][i];
+        vec[i] = c[l][k][i];
+    }
+    t = sqrt(t);
+    if (t <= 0) return;
+    for (int i = 0; i < dim; ++i) vec[i] /= t;
+}
+
+static void project(double data[][4], int n, const double *v, double *out, int dim)
+{
+    for (int k = 0; k < n; ++k) {
+        out[k] = 0;
+        for (int i = 0; i < dim; ++i) out[k] += data[k][i] * v[i];
+    }
+}
+
+/* quant_AnD_Shell, amd_bc7_3dquant_vpc.cpp:1201-1286 */
+static void lattice_round(const double *v_, int k, int n, int *idx)
+{
+    double v[64], z[64];
+    keyed d[64];
+    double m = v_[0], M = v_[0], dm = 0., r = 0;
+    for (int i = 1; i < n; ++i) {
+        m = m < v_[i] ? m : v_[i];
+        M = M > v_[i] ? M : v_[i];
+    }
+    if (M == m) {
+        for (int i = 0; i < n; ++i) idx[i] = 0;
+        return;
+    }
+    double s = (k - 1) / (M - m);
+    for (int i = 0; i < n; ++i) {
+        v[i] = v_[i] * s;
+        idx[i] = (int)(z[i] = floor(v[i] + 0.5 - m * s));
+        d[i].d = v[i] - z[i] - m * s;
+        d[i].i = i;
+        dm += d[i].d;
+        r += d[i].d * d[i].d;
+    }
+    if (n * r - dm * dm >= (double)(n - 1) / 4 / 2) {
+        dm /= (double)n;
+        for (int i = 0; i < n; ++i) d[i].d -= dm;
+        stable_sort(d, n);
+        for (int i = 0; i < n; ++i) d[i].d -= (2. * (double)i + 1 - (double)n) / 2. / (double)n;
+        double mm = 0., l = 0.;
+        int j = -1;
+        for (int i = 0; i < n; ++i) {
+            l += d[i].d;
+            if (l < mm) {
+                mm = l;
+                j = i;
+            }
+        }
+        j = (j + 1) % n;
+        for (int i = j; i < n; ++i) idx[d[i].i]++;
+    }
+    int mi = idx[0];
+    for (int i = 1; i < n; ++i) mi = mi < idx[i] ? mi : idx[i];
+    for (int i = 0; i < n; ++i) idx[i] -= mi;
+}
+
+static double total_error(double a[][4], double b[][4], int n, int dim)
+{
+    double t = 0;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < dim; ++j) t += (a[i][j] - b[i][j]) * (a[i][j] - b[i][j]);
+    return t;
+}
+
+/* optQuantAnD_d, amd_bc7_3dquant_vpc.cpp:1874-2045 */
+static double opt_quant(double data[][4], int n, int ncl, int *index, double out[][4], int dim)
+{
+    int snap[64], order[64];
+    double cen[64][4], mean[4], cov[4][4], prj[64], dir[4] = {0, 0, 0, 0};
+    double s, t;
+    int try_two = 50;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < dim; ++j) cen[i][j] = data[i][j];
+    /* centerInPlace_d :205-225 */
+    for (int i = 0; i < dim; ++i) {
+        mean[i] = 0;
+        for (int k = 0; k < n; ++k) mean[i] += cen[k][i];
+    }
+    if (n) {
+        for (int i = 0; i < dim; ++i) {
+            mean[i] /= (double)n;
+            for (int k = 0; k < n; ++k) cen[k][i] -= mean[i];
+        }
+    }
+    /* covariance_d :168-183 */
+    for (int i = 0; i < dim; ++i)
+        for (int j = 0; j <= i; ++j) {
+            cov[i][j] = 0;
+            for (int k = 0; k < n; ++k) cov[i][j] += cen[k][i] * cen[k][j];
+        }
+    for (int i = 0; i < dim; ++i)
+        for (int j = i + 1; j < dim; ++j) cov[i][j] = cov[j][i];
+    t = 0;
+    for (int j = 0; j < dim; ++j) t += cov[j][j];
+    if (t < (1. / 256.) || n == 0) {
+        for (int i = 0; i < n; ++i) {
+            index[i] = 0;
+            for (int j = 0; j < dim; ++j) out[i][j] = mean[j];
+        }
+        return 0.;
+    }
+    principal_vector(cov, dir, dim);
+    project(cen, n, dir, prj, dim);
+    for (int it = 0; it < 200; ++it) {
+        if (it) {
+            int done;
+            do {
+                double q = 0;
+                s = t = 0;
+                for (int k = 0; k < n; ++k) {
+                    s += index[k];
+                    t += index[k] * index[k];
+                }
+                for (int j = 0; j < dim; ++j) {
+                    dir[j] = 0;
+                    for (int k = 0; k < n; ++k) dir[j] += cen[k][j] * index[k];
+                    q += dir[j] * dir[j];
+                }
+                s /= (double)n;
+                t = t - s * s * (double)n;
+                t = (t == 0 ? 0. : 1 / t);
+                q = sqrt(q);
+                t *= q;
+                if (q != 0)
+                    for (int j = 0; j < dim; ++j) dir[j] /= q;
+                project(cen, n, dir, prj, dim);
+                sort_order(prj, order, n);
+                int nidx[64], k = 0;
+                for (int j = 0; j < n; ++j) {
+                    while (prj[order[j]] > (k + 0.5 - s) * t && k < ncl - 1) k++;
+                    nidx[order[j]] = k;
+                }
+                done = 1;
+                for (int j = 0; j < n; ++j) {
+                    done = (done && (nidx[j] == index[j]));
+                    index[j] = nidx[j];
+                }
+            } while (!done && try_two--);
+            if (it == 1) {
+                for (int j = 0; j < n; ++j) snap[j] = index[j];
+            } else {
+                /* Q5: compares against the it==1 snapshot, never refreshed (:1993-1998) */
+                done = 1;
+                for (int j = 0; j < n; ++j) done = (done && (snap[j] == index[j]));
+                if (done) break;
+            }
+        }
+        lattice_round(prj, ncl, n, index);
+    }
+    double q = 0;
+    s = t = 0;
+    for (int k = 0; k < n; ++k) {
+        s += index[k];
+        t += index[k] * index[k];
+    }
+    for (int j = 0; j < dim; ++j) {
+        dir[j] = 0;
+        for (int k = 0; k < n; ++k) dir[j] += cen[k][j] * index[k];
+        q += dir[j] * dir[j];
+    }
+    s /= (double)n;
+    t = t - s * s * (double)n;
+    t = (t == 0 ? 0. : 1 / t);
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < dim; ++j) out[i][j] = mean[j] + dir[j] * t * (index[i] - s);
+    return total_error(data, out, n, dim);
+}
+
+/* -------------------------------------------------------- shakers --- */
+
+/* index_collapse_, amd_shake.cpp:513-538 */
+static void collapse(int *idx, int n)
+{
+    if (!n) return;
+    int mi = idx[0], Mi = idx[0], D = 1;
+    for (int k = 1; k < n; ++k) {
+        mi = mi < idx[k] ? mi : idx[k];
+        Mi = Mi > idx[k] ? Mi : idx[k];
+    }
+    for (int d = 2; d <= Mi - mi; ++d) {
+        int k;
+        for (k = 0; k < n; ++k)
+            if ((idx[k] - mi) % d != 0) break;
+        if (k >= n) D = d;
+    }
+    for (int k = 0; k < n; ++k) idx[k] = (idx[k] - mi) / D;
+}
+
+static int max_index(const int *a, int n)
+{
+    int m = a[0];
+    for (int i = 0; i < n; ++i) m = m > a[i] ? m : a[i];
+    return m;
+}
+
+static int all_same(double d[][4], int n, int dim)
+{
+    int same = 1;
+    for (int i = 1; i < n; ++i)
+        for (int j = 0; j < dim; ++j) same = same && (d[0][j] == d[i][j]);
+    return same;
+}
+
+static void mean_of(double d[][4], double mean[4], int n, int dim)
+{
+    for (int j = 0; j < dim; ++j) mean[j] = 0;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < dim; ++j) mean[j] += d[i][j];
+    for (int j = 0; j < dim; ++j) mean[j] /= (double)n;
+}
+
+/* quant_single_point_d, amd_shake.cpp:546-701.  point = data[0]. */
+static double single_point(const double point[4], int n, int *index, double out[][4], int epo1[2][4],
+                           int last, const int *bits, int type, int dim)
+{
+    double err0 = DBL_MAX, err1 = DBL_MAX;
+    int idx = 0, idx1 = 0, epo0[2][4] = {{0}};
+    const int use_par = (type != 0);
+    const int clog = clog_of(last), c = clog - 2;
+    for (int pn = 0; pn < kParCount[type]; ++pn) {
+        int o1[2][4], o2[2][4];
+        for (int j = 0; j < dim; ++j) {
+            o2[0][j] = o1[0][j] = 0;
+            o2[1][j] = o1[1][j] = 2;
+            if (use_par) {
+                const int pv0 = kParVec[type][pn][0], pv1 = kParVec[type][pn][1];
+                if (pv0) o1[0][j] = 1; else o1[1][j] = 1;
+                if (pv1) o2[0][j] = 1; else o2[1][j] = 1;
+            }
+        }
+        for (int i = 0; i < (1 << clog); ++i) {
+            double t = 0;
+            int t1o[4] = {0}, t2o[4] = {0}, dr0[4] = {0};
+            for (int j = 0; j < dim; ++j) {
+                double tbest = DBL_MAX;
+                const int b = bits[j] - 5;
+                for (int t1 = o1[0][j]; t1 < o1[1][j]; ++t1)
+                    for (int t2 = o2[0][j]; t2 < o2[1][j]; ++t2) {
+                        int tf = (int)floor(point[j]);
+                        int tc = (int)ceil(point[j]);
+                        int dr;
+                        tf = (tf < 0) ? 0 : tf;
+                        tc = (tc > 255) ? 255 : tc;
+                        if (g_sp_err[c][b][tf][t1][t2][i] > g_sp_err[c][b][tc][t1][t2][i])
+                            dr = tc;
+                        else if (g_sp_err[c][b][tf][t1][t2][i] < g_sp_err[c][b][tc][t1][t2][i])
+                            dr = tf;
+                        else
+                            dr = (int)floor(point[j] + 0.5);
+                        double e = g_sp_err[c][b][dr][t1][t2][i];
+                        double tr = e + 2 * sqrt(e) * fabs((double)dr - point[j]) +
+                                    (dr - point[j]) * (dr - point[j]);
+                        if (tr < tbest) {
+                            tbest = tr;
+                            t1o[j] = t1;
+                            t2o[j] = t2;
+                            dr0[j] = dr;
+                        }
+                    }
+                t += tbest;
+            }
+            if (t < err0) {
+                idx = i;
+                for (int j = 0; j < dim; ++j) {
+                    epo0[0][j] = g_sp_idx[c][bits[j] - 5][dr0[j]][t1o[j]][t2o[j]][i][0];
+                    epo0[1][j] = g_sp_idx[c][bits[j] - 5][dr0[j]][t1o[j]][t2o[j]][i][1];
+                }
+                err0 = t;
+            }
+            if (err0 == 0) break;
+        }
+        if (err0 < err1) {
+            idx1 = idx;
+            for (int j = 0; j < dim; ++j) {
+                epo1[0][j] = epo0[0][j];
+                epo1[1][j] = epo0[1][j];
+            }
+            err1 = err0;
+        }
+        if (err1 == 0) break;
+    }
+    for (int i = 0; i < n; ++i) {
+        index[i] = idx1;
+        for (int j = 0; j < dim; ++j) out[i][j] = shake_ramp(clog, bits[j], epo1[0][j], epo1[1][j], idx1);
+    }
+    return err1 * n;
+}
+
+/* least-squares endpoints for an expanded index set (shared by both shakers,
+ * amd_shake.cpp:837-886 and :1169-1219) */
+static void ls_endpoints(double data[][4], const int *cidx, int n, int last, int dim, double epa[2][4])
+{
+    double im[2][2] = {{0, 0}, {0, 0}}, rp[2][4], cc[16][4];
+    int cnt[16], comp[16], ncl = 0;
+    /* cluster_mean_d_d :445-472 */
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < dim; ++j) {
+            cc[cidx[i]][j] = 0;
+            cnt[cidx[i]] = 0;
+        }
+    for (int i = 0; i < n; ++i) {
+        for (int j = 0; j < dim; ++j) cc[cidx[i]][j] += data[i][j];
+        if (cnt[cidx[i]] == 0) comp[ncl++] = cidx[i];
+        cnt[cidx[i]]++;
+    }
+    for (int i = 0; i < ncl; ++i)
+        for (int j = 0; j < dim; ++j) cc[comp[i]][j] /= (double)cnt[comp[i]];
+    for (int i = 0; i < ncl; ++i)
+        for (int j = 0; j < dim; ++j) cc[comp[i]][j] = floor(cc[comp[i]][j] + 0.5);
+    for (int j = 0; j < dim; ++j) rp[0][j] = rp[1][j] = 0;
+    for (int k = 0; k < n; ++k) {
+        im[0][0] += (last - cidx[k]) * (last - cidx[k]);
+        im[0][1] += cidx[k] * (last - cidx[k]);
+        im[1][1] += cidx[k] * cidx[k];
+        for (int j = 0; j < dim; ++j) {
+            rp[0][j] += (last - cidx[k]) * cc[cidx[k]][j];
+            rp[1][j] += cidx[k] * cc[cidx[k]][j];
+        }
+    }
+    double dd = im[0][0] * im[1][1] - im[0][1] * im[0][1];
+    im[1][0] = im[0][0];
+    im[0][0] = im[1][1] / dd;
+    im[1][1] = im[1][0] / dd;
+    im[1][0] = im[0][1] = -im[0][1] / dd;
+    for (int j = 0; j < dim; ++j) {
+        epa[0][j] = (im[0][0] * rp[0][j] + im[0][1] * rp[1][j]) * last;
+        epa[1][j] = (im[1][0] * rp[0][j] + im[1][1] * rp[1][j]) * last;
+    }
+}
+
+/* ep_shaker_2_d, amd_shake.cpp:703-1053.  index_ updated in place. */
+static double shake_window(double data[][4], int n, int *index_, int epo_code[2][4], int size, int last,
+                           int bits, int dim)
+{
+    const int type = bits % (2 * dim);
+    const int use_par = (type != 0);
+    int mb[4];
+    for (int j = 0; j < dim; ++j) mb[j] = (bits + 2 * dim - 1) / (2 * dim);
+    const int clog = clog_of(last);
+    double mean[4], err_o = DBL_MAX, outg[16][4];
+    int index[16], epo0[2][4] = {{0}};
+    int max_try = 8, done;
+    for (int k = 0; k < n; ++k) index[k] = index_[k];
+    const int alls = all_same(data, n, dim);
+    mean_of(data, mean, n, dim);
+    do {
+        collapse(index, n);
+        const int Mi = max_index(index, n);
+        int p0 = -1, q0 = -1;
+        double err0 = DBL_MAX;
+        if (Mi == 0) {
+            double t;
+            if (alls) {
+                t = single_point(data[0], n, index, outg, epo0, last, mb, type, dim);
+            } else {
+                single_point(mean, n, index, outg, epo0, last, mb, type, dim);
+                t = total_error(data, outg, n, dim);
+            }
+            if (t < err_o) {
+                for (int k = 0; k < n; ++k) {
+                    index_[k] = index[k];
+                    for (int j = 0; j < dim; ++j) {
+                        epo_code[0][j] = epo0[0][j];
+                        epo_code[1][j] = epo0[1][j];
+                    }
+                }
+                err_o = t;
+            }
+            return err_o;
+        }
+        for (int q = 1; q * Mi <= last; ++q)
+            for (int p = 0; p <= last - q * Mi; ++p) {
+                int cidx[16];
+                double epa[2][4];
+                for (int k = 0; k < n; ++k) cidx[k] = index[k] * q + p;
+                ls_endpoints(data, cidx, n, last, dim, epa);
+                double err1 = DBL_MAX, ed[2][2][4];
+                int epo1[2][4], best2[2][2][2][4];
+                for (int j = 0; j < dim; ++j) {
+                    const int rr = use_par ? 2 : 1;
+                    for (int a = 0; a < rr; ++a)
+                        for (int b = 0; b < rr; ++b) {
+                            int lo[2], hi[2], pp[2] = {a, b};
+                            for (int i = 0; i < 2; ++i) {
+                                int f = ep_floor(epa[i][j], mb[j], use_par, pp[i]);
+                                lo[i] = hi[i] = f;
+                                lo[i] -= ((f < (size >> 1) - 1) ? f : (size >> 1) - 1) & (~use_par);
+                                hi[i] += (((1 << mb[j]) - 1 - f < (size >> 1)) ? (1 << mb[j]) - 1 - f
+                                                                                  : (size >> 1)) &
+                                         (~use_par);
+                            }
+                            const int step = 1 << use_par;
+                            ed[a][b][j] = DBL_MAX;
+                            for (int p1 = lo[0]; p1 <= hi[0]; p1 += step)
+                                for (int p2 = lo[1]; p2 <= hi[1]; p2 += step) {
+                                    double t = 0;
+                                    for (int m = n; m > 0; --m) {
+                                        double rv = shake_ramp(clog, mb[j], p1, p2, cidx[m - 1]);
+                                        t += (rv - data[m - 1][j]) * (rv - data[m - 1][j]);
+                                    }
+                                    if (t < ed[a][b][j]) {
+                                        ed[a][b][j] = t;
+                                        best2[a][b][0][j] = p1;
+                                        best2[a][b][1][j] = p2;
+                                    }
+                                }
+                        }
+                }
+                for (int pn = 0; pn < kParCount[type]; ++pn) {
+                    const int v0 = kParVec[type][pn][0], v1 = kParVec[type][pn][1];
+                    double e2 = 0;
+                    for (int j = 0; j < dim; ++j) e2 += ed[v0][v1][j];
+                    if (e2 < err1) {
+                        err1 = e2;
+                        for (int j = 0; j < dim; ++j) {
+                            epo1[0][j] = best2[v0][v1][0][j];
+                            epo1[1][j] = best2[v0][v1][1][j];
+                        }
+                    }
+                }
+                if (err1 <= err0) { /* Q7: last minimum wins */
+                    err0 = err1;
+                    p0 = p;
+                    q0 = q;
+                    for (int j = 0; j < dim; ++j) {
+                        epo0[0][j] = epo1[0][j];
+                        epo0[1][j] = epo1[1][j];
+                    }
+                }
+            }
+        /* requantize :980-1018 */
+        int idg[16];
+        double err_r = 0;
+        for (int i = 0; i < n; ++i) {
+            double cmin = DBL_MAX;
+            int ci = 0;
+            for (int j = 0; j < (1 << clog); ++j) {
+                double t = 0.;
+                for (int k = 0; k < dim; ++k) {
+                    double rv = shake_ramp(clog, mb[k], epo0[0][k], epo0[1][k], j);
+                    t += (rv - data[i][k]) * (rv - data[i][k]);
+                }
+                if (t < cmin) {
+                    cmin = t;
+                    ci = j;
+                }
+            }
+            idg[i] = ci;
+            err_r += cmin;
+        }
+        int change = 0;
+        for (int k = 0; k < n; ++k) change = change || (index[k] * q0 + p0 != idg[k]);
+        const int better = err_r < err_o;
+        if (better) {
+            for (int k = 0; k < n; ++k) {
+                index_[k] = index[k] = idg[k];
+                for (int j = 0; j < dim; ++j) {
+                    epo_code[0][j] = epo0[0][j];
+                    epo_code[1][j] = epo0[1][j];
+                }
+            }
+            err_o = err_r;
+        }
+        done = !(change && better);
+    } while (!done && max_try--);
+    return err_o;
+}
+
+/* ep_shaker_d, amd_shake.cpp:1058-1404 (dimension 3 only).  index_ and
+ * epo_code updated in place. */
+static double shake_corners(double data[][4], int n, int *index_, int epo_code[2][4], int last,
+                            const int *bits, int type, int dim)
+{
+    const int use_par = (type == PAR_BCC || type == PAR_SAME);
+    const int bcc = (type == PAR_BCC);
+    const int clog = clog_of(last), nc = 1 << clog;
+    double mean[4], err_o = DBL_MAX;
+    int index[16], max_try = 1, done;
+    for (int k = 0; k < n; ++k) index[k] = index_[k];
+    const int alls = all_same(data, n, dim);
+    mean_of(data, mean, n, dim);
+    do {
+        collapse(index, n);
+        const int Mi = max_index(index, n);
+        int p0 = -1, q0 = -1, idx2[16] = {0}, epo2[2][4] = {{0}};
+        double err2 = DBL_MAX;
+        if (Mi == 0) {
+            double t, o2[16][4];
+            int epo0[2][4] = {{0}};
+            if (alls) {
+                t = single_point(data[0], n, index, o2, epo0, last, bits, type, dim);
+            } else {
+                single_point(mean, n, index, o2, epo0, last, bits, type, dim);
+                t = total_error(data, o2, n, dim);
+            }
+            if (t < err_o) {
+                for (int k = 0; k < n; ++k) {
+                    index_[k] = index[k];
+                    for (int j = 0; j < dim; ++j) {
+                        epo_code[0][j] = epo0[0][j];
+                        epo_code[1][j] = epo0[1][j];
+                    }
+                }
+                err_o = t;
+            }
+            return err_o;
+        }
+        for (int q = 1; q * Mi <= last; ++q)
+            for (int p = 0; p <= last - q * Mi; ++p) {
+                int cidx[16], idx1[16] = {0}, epo1[2][4] = {{0}}, s1 = 0;
+                double epa[2][4], err1 = DBL_MAX;
+                for (int k = 0; k < n; ++k) cidx[k] = index[k] * q + p;
+                ls_endpoints(data, cidx, n, last, dim, epa);
+                for (int odd = 0; odd <= use_par; ++odd)
+                    for (int flip = 0; flip <= bcc; ++flip) {
+                        int epi[2][4][2];
+                        for (int j = 0; j < dim; ++j)
+                            for (int i = 0; i < 2; ++i) {
+                                int f = ep_floor(epa[i][j], bits[j], use_par, (odd ^ (flip & i)) & 1);
+                                epi[i][j][0] = epi[i][j][1] = f;
+                                epi[i][j][1] += (((1 << bits[j]) - 1 - f < (1 << use_par))
+                                                     ? (1 << bits[j]) - 1 - f
+                                                     : (1 << use_par)) &
+                                                (~use_par);
+                            }
+                        /* 64-corner Gray-code walk :1273-1341; evaluated per corner */
+                        int s = 0;
+                        for (int p1 = 0; p1 < 64; ++p1) {
+                            const int g = p1 & (-p1);
+                            s ^= g;
+                            double r[4][16];
+                            for (int j = 0; j < dim; ++j) {
+                                const int e0 = (s >> (2 * j)) & 1, e1 = (s >> (2 * j + 1)) & 1;
+                                for (int c = 0; c < nc; ++c)
+                                    r[j][c] = shake_ramp(clog, bits[j], epi[0][j][e0], epi[1][j][e1], c);
+                            }
+                            double err0 = 0;
+                            int idx0[16];
+                            for (int i = 0; i < n; ++i) {
+                                int ci = 0;
+                                double cmin = DBL_MAX;
+                                for (int c = 0; c < nc; ++c) {
+                                    double t = 0.;
+                                    for (int k = 0; k < dim; ++k)
+                                        t += (r[k][c] - data[i][k]) * (r[k][c] - data[i][k]);
+                                    if (t < cmin) {
+                                        cmin = t;
+                                        ci = c;
+                                    }
+                                }
+                                idx0[i] = ci;
+                                err0 += cmin;
+                            }
+                            if (err0 < err1) {
+                                for (int i = 0; i < n; ++i) idx1[i] = idx0[i];
+                                err1 = err0;
+                                s1 = s;
+                            }
+                        }
+                        /* Q6: rebuilt from the global s1 and this pass's ranges */
+                        for (int j = 0; j < dim; ++j) {
+                            epo1[0][j] = epi[0][j][(s1 >> (2 * j)) & 1];
+                            epo1[1][j] = epi[1][j][(s1 >> (2 * j + 1)) & 1];
+                        }
+                    }
+                if (err1 < err2) {
+                    for (int i = 0; i < n; ++i) idx2[i] = idx1[i];
+                    err2 = err1;
+                    for (int j = 0; j < dim; ++j) {
+                        epo2[0][j] = epo1[0][j];
+                        epo2[1][j] = epo1[1][j];
+                    }
+                    p0 = p;
+                    q0 = q;
+                }
+            }
+        int change = 0;
+        for (int k = 0; k < n; ++k) change = change || (index[k] * q0 + p0 != idx2[k]);
+        const int better = err2 < err_o;
+        if (better) {
+            for (int k = 0; k < n; ++k) {
+                index_[k] = index[k] = idx2[k];
+                for (int j = 0; j < dim; ++j) {
+                    epo_code[0][j] = epo2[0][j];
+                    epo_code[1][j] = epo2[1][j];
+                }
+            }
+            err_o = err2;
+        }
+        done = !(change && better);
+    } while (!done && max_try--);
+    return err_o;
+}
+
+/* ------------------------------------------------------ block encode --- */
+typedef struct {
+    double quality, performance, quant_thr, shake_thr, part_search, err_thr, max_range;
+    int colour_restrict, alpha_restrict;
+    unsigned valid_mask;
+    int parity, clusters[2], cbits[4];
+    int stored[64][3][16];
+    double stored_err[64];
+    int sorted[64];
+    int unsupported;
+} bc7_enc;
+
+static void put_bits(uint8_t *blk, int *pos, unsigned v, int n)
+{
+    for (int i = 0; i < n; ++i, ++*pos) {
+        const int byte = *pos >> 3, bit = *pos & 7;
+        blk[byte] = (uint8_t)((blk[byte] & ~(1u << bit)) | (((v >> i) & 1u) << bit));
+    }
+}
+
+static unsigned shape_of(int subsets, int part, int texel)
+{
+    if (subsets == 1) return 0;
+    const unsigned m = subsets == 2 ? kBc7Shape2[part] : kBc7Shape3[part];
+    return (m >> (2 * texel)) & 3u;
+}
+
+/* Partition, amd_bc7_partitions.cpp:1007-1053 */
+static void split_subsets(int part, double in[16][4], double sub[3][16][4], int cnt[3], int subsets,
+                          int dim)
+{
+    cnt[0] = cnt[1] = cnt[2] = 0;
+    for (int i = 0; i < 16; ++i) {
+        const int s = (int)shape_of(subsets, part, i);
+        for (int j = 0; j < dim; ++j) sub[s][cnt[s]][j] = in[i][j];
+        if (dim < 4) sub[s][cnt[s]][dim] = 0.0;
+        cnt[s]++;
+    }
+}
+
+/* BlockSetup, amd_bc7_body.cpp:270-324 */
+static void mode_setup(bc7_enc *e, int mode)
+{
+    const mode_info *mi = &kModes[mode];
+    e->parity = mi->pbit == 0 ? PAR_CART : mi->pbit == 1 ? PAR_SAME : PAR_BCC;
+    if (mi->enc == ENC_NO_ALPHA) {
+        e->cbits[0] = e->cbits[1] = e->cbits[2] = mi->vector_bits / 3;
+        e->cbits[3] = 0;
+        e->clusters[0] = 1 << mi->ib0;
+        e->clusters[1] = 0;
+    } else if (mi->enc == ENC_COMBINED) {
+        e->cbits[0] = e->cbits[1] = e->cbits[2] = e->cbits[3] = mi->vector_bits / 4;
+        e->clusters[0] = 1 << mi->ib0;
+        e->clusters[1] = 0;
+    } else {
+        e->cbits[0] = e->cbits[1] = e->cbits[2] = mi->vector_bits / 3;
+        e->cbits[3] = mi->scalar_bits;
+        e->clusters[0] = 1 << mi->ib0;
+        e->clusters[1] = 1 << mi->ib1;
+    }
+}
+
+static int anchor_of(int subsets, int part, int s)
+{
+    if (s == 0) return 0;
+    if (subsets == 2) return kBc7Anchor2[part];
+    return s == 1 ? kBc7Anchor3a[part] : kBc7Anchor3b[part];
+}
+
+/* EncodeSingleIndexBlock, amd_bc7_body.cpp:333-538 */
+static void pack_single(const bc7_enc *e, int mode, int part, unsigned colour[3][2], int idx[3][16],
+                        uint8_t out[16])
+{
+    const mode_info *mi = &kModes[mode];
+    int pos = 0, cnt[3] = {0, 0, 0}, flip[3] = {0, 0, 0};
+    unsigned bidx[16];
+    put_bits(out, &pos, 1u << mode, mode + 1);
+    put_bits(out, &pos, (unsigned)part, mi->part_bits);
+    for (int i = 0; i < 16; ++i) {
+        const int s = (int)shape_of(mi->subsets, part, i);
+        bidx[i] = (unsigned)idx[s][cnt[s]++];
+        for (int j = 0; j < mi->subsets; ++j)
+            if (i == anchor_of(mi->subsets, part, j) && (bidx[i] & (1u << (mi->ib0 - 1)))) flip[j] = 1;
+    }
+    for (int s = 0; s < mi->subsets; ++s)
+        if (flip[s]) {
+            unsigned t = colour[s][0];
+            colour[s][0] = colour[s][1];
+            colour[s][1] = t;
+        }
+    for (int i = 0; i < 16; ++i)
+        if (flip[shape_of(mi->subsets, part, i)]) bidx[i] = ((1u << mi->ib0) - 1) - bidx[i];
+    unsigned comp[3][2][4], par[3][2];
+    for (int s = 0; s < mi->subsets; ++s) {
+        unsigned pc[2] = {colour[s][0], colour[s][1]};
+        if (mi->pbit == 2) {
+            par[s][0] = pc[0] & 1;
+            par[s][1] = pc[1] & 1;
+            pc[0] >>= 1;
+            pc[1] >>= 1;
+        } else if (mi->pbit == 1) {
+            par[s][0] = pc[1] & 1;
+            par[s][1] = pc[1] & 1;
+            pc[0] >>= 1;
+            pc[1] >>= 1;
+        } else {
+            par[s][0] = par[s][1] = 0;
+        }
+        for (int c = 0; c < 4; ++c)
+            if (e->cbits[c]) {
+                comp[s][0][c] = pc[0] & ((1u << e->cbits[c]) - 1);
+                comp[s][1][c] = pc[1] & ((1u << e->cbits[c]) - 1);
+                pc[0] >>= e->cbits[c];
+                pc[1] >>= e->cbits[c];
+            }
+    }
+    for (int c = 0; c < 4; ++c)
+        for (int s = 0; s < mi->subsets; ++s)
+            for (int ep = 0; ep < 2; ++ep) put_bits(out, &pos, comp[s][ep][c], e->cbits[c]);
+    if (mi->pbit)
+        for (int s = 0; s < mi->subsets; ++s) {
+            put_bits(out, &pos, par[s][0], 1);
+            if (mi->pbit == 2) put_bits(out, &pos, par[s][1], 1);
+        }
+    for (int i = 0; i < 16; ++i) {
+        const int s = (int)shape_of(mi->subsets, part, i);
+        put_bits(out, &pos, bidx[i], i == anchor_of(mi->subsets, part, s) ? mi->ib0 - 1 : mi->ib0);
+    }
+}
+
+/* CompressSingleIndexBlock, amd_bc7_body.cpp:548-890 */
+static double single_index(bc7_enc *e, double in[16][4], uint8_t out[16], int mode)
+{
+    const mode_info *mi = &kModes[mode];
+    const int dim = mi->enc == ENC_NO_ALPHA ? 3 : 4;
+    const unsigned nparts = 1u << mi->part_bits;
+    unsigned tries = nparts;
+    if (e->quality < 0.5) {
+        tries = (unsigned)floor((double)(tries * e->part_search) + 0.5);
+        tries = tries < 1 ? 1 : tries;
+        tries = tries > nparts ? nparts : tries;
+    }
+    double sub[3][16][4];
+    int cnt[3];
+    for (unsigned part = 0; part < tries; ++part) {
+        split_subsets((int)part, in, sub, cnt, mi->subsets, dim);
+        double err = 0.;
+        for (int s = 0; s < mi->subsets; ++s) {
+            if (!cnt[s]) continue;
+            int idx[16];
+            double o[16][4];
+            if (e->clusters[0] > 8 || e->max_range <= e->quant_thr) {
+                err += opt_quant(sub[s], cnt[s], e->clusters[0], idx, o, dim);
+            } else {
+                e->unsupported = 1;
+                return DBL_MAX;
+            }
+            for (int k = 0; k < cnt[s]; ++k) e->stored[part][s][k] = idx[k];
+        }
+        e->stored_err[part] = err;
+    }
+    sort_order(e->stored_err, e->sorted, (int)tries);
+
+    int bits[4] = {0, 0, 0, 0};
+    bits[0] = e->cbits[0] + (e->parity ? 1 : 0);
+    bits[1] = e->cbits[1] + (e->parity ? 1 : 0);
+    bits[2] = e->cbits[2] + (e->parity ? 1 : 0);
+    for (int i = 0; i < dim; ++i) bits[3] += e->cbits[i];
+    bits[3] *= 2;
+    if (e->parity == PAR_BCC)
+        bits[3] += 2;
+    else if (e->parity == PAR_SAME)
+        bits[3] += 1;
+
+    unsigned shake = 8 - (unsigned)floor(1.5 * mi->ib0);
+    {
+        unsigned t = (unsigned)floor(shake * e->quality + 0.5);
+        t = t < 6 ? t : 6;
+        shake = t > 2 ? t : 2;
+    }
+    unsigned attempts = (unsigned)floor(8 * e->quality + 0.5);
+    attempts = attempts < tries ? attempts : tries;
+    attempts = attempts > 1 ? attempts : 1;
+    if (e->parity == PAR_SAME || e->parity == PAR_BCC) shake += 2;
+
+    int epo_code[3][2][4], best_ep[3][2][4], best_idx[3][16], best_cnt[3] = {0, 0, 0};
+    unsigned best_part = 0;
+    double best_err = DBL_MAX;
+    memset(epo_code, 0, sizeof(epo_code));
+    memset(best_ep, 0, sizeof(best_ep));
+    for (unsigned i = 0; i < attempts; ++i) {
+        double err = 0;
+        const int part = e->sorted[i];
+        split_subsets(part, in, sub, cnt, mi->subsets, dim);
+        for (int s = 0; s < mi->subsets; ++s) {
+            if (!cnt[s]) continue;
+            if (e->max_range > e->shake_thr || dim != 3) {
+                err += shake_window(sub[s], cnt[s], e->stored[part][s], epo_code[s], (int)shake,
+                                    e->clusters[0] - 1, bits[3], dim);
+            } else {
+                int tidx[16], tepo[2][4];
+                double te[2];
+                memset(tepo, 0, sizeof(tepo));
+                for (int k = 0; k < cnt[s]; ++k) tidx[k] = e->stored[part][s][k];
+                te[0] = shake_corners(sub[s], cnt[s], tidx, tepo, e->clusters[0] - 1, bits, e->parity, dim);
+                te[1] = shake_window(sub[s], cnt[s], e->stored[part][s], epo_code[s], (int)shake,
+                                     e->clusters[0] - 1, bits[3], dim);
+                if (te[0] < te[1]) {
+                    te[1] = shake_window(sub[s], cnt[s], tidx, tepo, (int)shake, e->clusters[0] - 1,
+                                         bits[3], dim);
+                    for (int k = 0; k < cnt[s]; ++k) e->stored[part][s][k] = tidx[k];
+                    for (int k = 0; k < 4; ++k) {
+                        epo_code[s][0][k] = tepo[0][k];
+                        epo_code[s][1][k] = tepo[1][k];
+                    }
+                }
+                err += te[1];
+            }
+        }
+        if (err < best_err) {
+            best_part = (unsigned)part;
+            for (int s = 0; s < mi->subsets; ++s) {
+                best_cnt[s] = cnt[s];
+                if (cnt[s]) {
+                    for (int k = 0; k < dim; ++k) {
+                        best_ep[s][0][k] = epo_code[s][0][k];
+                        best_ep[s][1][k] = epo_code[s][1][k];
+                    }
+                    for (int k = 0; k < cnt[s]; ++k) best_idx[s][k] = e->stored[part][s][k];
+                }
+            }
+            best_err = err;
+        }
+        if (e->err_thr > 0 && best_err <= e->err_thr) break;
+    }
+    unsigned packed[3][2] = {{0, 0}, {0, 0}, {0, 0}};
+    for (int s = 0; s < mi->subsets; ++s) {
+        if (!best_cnt[s]) continue;
+        int shift = 0;
+        if (e->parity != PAR_CART) {
+            packed[s][0] = (unsigned)best_ep[s][0][0] & 1;
+            packed[s][1] = (unsigned)best_ep[s][1][0] & 1;
+            for (int k = 0; k < 4; ++k) {
+                best_ep[s][0][k] >>= 1;
+                best_ep[s][1][k] >>= 1;
+            }
+            shift++;
+        }
+        for (int k = 0; k < dim; ++k)
+            if (e->cbits[k]) {
+                packed[s][0] |= (unsigned)best_ep[s][0][k] << shift;
+                packed[s][1] |= (unsigned)best_ep[s][1][k] << shift;
+                shift += e->cbits[k];
+            }
+    }
+    pack_single(e, mode, (int)best_part, packed, best_idx, out);
+    return best_err;
+}
+
+static const int kRot[4][4] = {{3, 0, 1, 2}, {0, 3, 1, 2}, {1, 0, 3, 2}, {2, 0, 1, 3}};
+
+/* EncodeDualIndexBlock, amd_bc7_body.cpp:902-1056 */
+static void pack_dual(int mode, int sel, int rot, int ep[2][2][4], int idx[2][16], uint8_t out[16])
+{
+    const mode_info *mi = &kModes[mode];
+    int pos = 0, ib[2], flip[2];
+    put_bits(out, &pos, 1u << mode, mode + 1);
+    put_bits(out, &pos, (unsigned)rot, mi->rot_bits);
+    put_bits(out, &pos, sel ? 1u : 0u, mi->idxmode_bits);
+    ib[0] = sel ? mi->ib1 : mi->ib0;
+    ib[1] = sel ? mi->ib0 : mi->ib1;
+    flip[0] = (idx[0][0] & (1 << (ib[0] - 1))) != 0;
+    flip[1] = (idx[1][0] & (1 << (ib[1] - 1))) != 0;
+    for (int i = 0; i < 2; ++i)
+        if (flip[i]) {
+            for (int j = 0; j < 16; ++j) idx[i][j] = ((1 << ib[i]) - 1) - idx[i][j];
+            for (int k = 0; k < 4; ++k) {
+                int t = ep[i][0][k];
+                ep[i][0][k] = ep[i][1][k];
+                ep[i][1][k] = t;
+            }
+        }
+    const int vb = mi->vector_bits / 3;
+    for (int c = 0; c < 4; ++c)
+        for (int e = 0; e < 2; ++e) {
+            if (c != 3)
+                put_bits(out, &pos, (unsigned)ep[0][e][c], vb);
+            else
+                put_bits(out, &pos, (unsigned)ep[1][e][0], mi->scalar_bits);
+        }
+    for (int i = 0; i < 2; ++i) {
+        const int s = sel ? i ^ 1 : i;
+        for (int j = 0; j < 16; ++j) put_bits(out, &pos, (unsigned)idx[s][j], j == 0 ? ib[s] - 1 : ib[s]);
+    }
+}
+
+/* CompressDualIndexBlock, amd_bc7_body.cpp:1059-1278 */
+static double dual_index(bc7_enc *e, double in[16][4], uint8_t out[16], int mode)
+{
+    const mode_info *mi = &kModes[mode];
+    const int nrot = 1 << mi->rot_bits, nsel = 1 << mi->idxmode_bits;
+    const int ibs[2] = {mi->ib0, mi->ib1};
+    double cb[16][4], ab[16][4], best_q = DBL_MAX, best_o = DBL_MAX;
+    int idx[2][16];
+    double oq[2][16][4];
+    for (int rot = 0; rot < nrot; ++rot) {
+        for (int i = 0; i < 16; ++i) {
+            cb[i][0] = in[i][kRot[rot][1]];
+            cb[i][1] = in[i][kRot[rot][2]];
+            cb[i][2] = in[i][kRot[rot][3]];
+            ab[i][0] = ab[i][1] = ab[i][2] = in[i][kRot[rot][0]];
+            cb[i][3] = ab[i][3] = 0.0;
+        }
+        for (int sel = 0; sel < nsel; ++sel) {
+            double qe = 0.;
+            if (!(e->max_range <= e->quant_thr)) {
+                e->unsupported = 1;
+                return DBL_MAX;
+            }
+            qe = opt_quant(cb, 16, 1 << ibs[sel], idx[0], oq[0], 3);
+            qe += opt_quant(ab, 16, 1 << ibs[1 ^ sel], idx[1], oq[1], 3) / 3.;
+            if (e->quality > 0.7 || qe <= best_q) {
+                unsigned shake = (unsigned)(6 * e->quality);
+                shake = shake < 6 ? shake : 6;
+                shake = shake > 2 ? shake : 2;
+                int bits[2][4];
+                bits[0][0] = bits[0][1] = bits[0][2] = e->cbits[0];
+                bits[0][3] = 2 * (e->cbits[0] + e->cbits[1] + e->cbits[2]);
+                bits[1][0] = bits[1][1] = bits[1][2] = e->cbits[3];
+                bits[1][3] = 6 * e->cbits[3];
+                double overall = 0;
+                int epo[2][2][4];
+                memset(epo, 0, sizeof(epo));
+                const int last0 = (1 << ibs[sel]) - 1, last1 = (1 << ibs[1 ^ sel]) - 1;
+                if (e->max_range > e->shake_thr) {
+                    overall += shake_window(cb, 16, idx[0], epo[0], (int)shake, last0, bits[0][3], 3);
+                } else {
+                    /* Q9: return ignored, in-place side effects kept */
+                    shake_corners(cb, 16, idx[0], epo[0], last0, bits[0], PAR_CART, 3);
+                    overall += shake_window(cb, 16, idx[0], epo[0], (int)shake, last0, bits[0][3], 3);
+                }
+                if (e->max_range > e->shake_thr) {
+                    overall += shake_window(ab, 16, idx[1], epo[1], (int)shake, last1, bits[1][3], 3) / 3.;
+                } else {
+                    shake_corners(ab, 16, idx[1], epo[1], last1, bits[1], PAR_CART, 3);
+                    overall += shake_window(ab, 16, idx[1], epo[1], (int)shake, last1, bits[1][3], 3) / 3.;
+                }
+                if (overall < best_o) {
+                    pack_dual(mode, sel, rot, epo, idx, out);
+                    best_o = overall;
+                }
+                if (qe < best_q) best_q = qe;
+            }
+        }
+    }
+    return best_o;
+}
+
+double orc_bc7_block(const float inN[64], uint8_t mode_mask, int src_has_alpha, float quality_f,
+                     int colour_restrict, int alpha_restrict, float performance_f, uint8_t out[16])
+{
+    (void)src_has_alpha; /* m_imageNeedsAlpha is never read by CompressBlock */
+    pthread_once(&g_once, build_tables);
+    static __thread bc7_enc enc;
+    bc7_enc *e = &enc;
+    memset(e, 0, sizeof(*e));
+    /* BC7BlockEncoder ctor, amd_bc7_body.hpp:94-149 */
+    e->valid_mask = mode_mask == 0 ? 0xCF : mode_mask;
+    double q = quality_f, pf = performance_f;
+    e->quality = q < 1.0 ? (q > 0.0 ? q : 0.0) : 1.0;
+    e->performance = pf < 1.0 ? (pf > 0.0 ? pf : 0.0) : 1.0;
+    e->colour_restrict = colour_restrict;
+    e->alpha_restrict = alpha_restrict;
+    e->quant_thr = 255 * e->performance;
+    if (e->quality < 0.5) {
+        e->shake_thr = 0.;
+        e->err_thr = 256. * (1.0 - ((e->quality * 2.0) / 0.5));
+        e->part_search = (1.0 / 16.0) > ((e->quality * 2.0) / 0.5) ? (1.0 / 16.0) : ((e->quality * 2.0) / 0.5);
+    } else if (e->quality < 0.7) {
+        e->shake_thr = 255 * (e->quality / 10);
+        e->err_thr = 256. * (1.0 - (e->quality / 0.5));
+        e->part_search = (1.0 / 16.0) > (e->quality / 0.5) ? (1.0 / 16.0) : (e->quality / 0.5);
+    } else {
+        e->shake_thr = 255 * e->quality;
+        e->err_thr = 0;
+        e->part_search = 1.0;
+    }
+    /* CompressBlock, amd_bc7_body.cpp:1289-1465 */
+    double in[16][4], bmin[4], bmax[4];
+    int needs_alpha = 0, zero_one = 0;
+    for (int j = 0; j < 4; ++j) {
+        bmin[j] = DBL_MAX;
+        bmax[j] = 0.0;
+    }
+    for (int i = 0; i < 16; ++i) {
+        if (inN[i * 4 + 3] < 1.0)
+            needs_alpha = 1;
+        else if ((inN[i * 4 + 3] >= 0.99999) || (inN[i * 4 + 3] < 0.00001))
+            zero_one = 1;
+        for (int j = 0; j < 4; ++j) {
+            in[i][j] = inN[i * 4 + j] * 255.0f; /* Q8: float multiply */
+            bmin[j] = (in[i][j] < bmin[j]) ? in[i][j] : bmin[j];
+            bmax[j] = (in[i][j] > bmax[j]) ? in[i][j] : bmax[j];
+        }
+    }
+    double mr = bmax[0] - bmin[0];
+    for (int j = 1; j < 4; ++j) mr = (bmax[j] - bmin[j]) > mr ? (bmax[j] - bmin[j]) : mr;
+    e->max_range = mr;
+    const int solid = mr < 1e-10;
+    unsigned valid = e->valid_mask;
+    for (int m = 0; m < 8; ++m) {
+        if (!(valid & (1u << m))) continue;
+        if (needs_alpha && kModes[m].enc == ENC_NO_ALPHA) valid &= ~(1u << m);
+        if (!solid && !needs_alpha && e->colour_restrict && kModes[m].enc == ENC_COMBINED) valid &= ~(1u << m);
+        if (needs_alpha && e->alpha_restrict && zero_one && kModes[m].enc == ENC_COMBINED) valid &= ~(1u << m);
+    }
+    static const int order[8] = {6, 4, 3, 1, 2, 0, 7, 5};
+    uint8_t tmp[16];
+    double best = DBL_MAX;
+    memset(tmp, 0, sizeof(tmp));
+    for (int k = 0; k < 8; ++k) {
+        const int m = order[k];
+        if (!(valid & (1u << m))) continue;
+        mode_setup(e, m);
+        double err = kModes[m].enc != ENC_SEPARATE ? single_index(e, in, tmp, m) : dual_index(e, in, tmp, m);
+        if (e->unsupported) return -1.0;
+        if (err < best) {
+            memcpy(out, tmp, 16);
+            best = err;
+        }
+        if (e->err_thr > 0 && best <= e->err_thr) break;
+    }
+    return best;
+}
+
+/* ----------------------------------------------------------- decoder --- */
+/* Standard BC7 decode (format spec) for tolerance checks. */
+static unsigned get_bits(const uint8_t *b, int *pos, int n)
+{
+    unsigned v = 0;
+    for (int i = 0; i < n; ++i, ++*pos) v |= (unsigned)((b[*pos >> 3] >> (*pos & 7)) & 1) << i;
+    return v;
+}
+
+void orc_bc7_decode(const uint8_t blk[16], uint8_t rgba[64])
+{
+    static const int w2[4] = {0, 21, 43, 64};
+    static const int w3[8] = {0, 9, 18, 27, 37, 46, 55, 64};
+    static const int w4[16] = {0, 4, 9, 13, 17, 21, 26, 30, 34, 38, 43, 47, 51, 55, 60, 64};
+    int mode = 0;
+    while (mode < 8 && !(blk[mode >> 3] & (1 << (mode & 7)))) mode++;
+    if (mode >= 8) {
+        memset(rgba, 0, 64);
+        return;
+    }
+    const mode_info *mi = &kModes[mode];
+    int pos = mode + 1;
+    const int part = (int)get_bits(blk, &pos, mi->part_bits);
+    const int rot = (int)get_bits(blk, &pos, mi->rot_bits);
+    const int sel = (int)get_bits(blk, &pos, mi->idxmode_bits);
+    const int ns = mi->subsets;
+    int cb = mi->enc == ENC_COMBINED ? mi->vector_bits / 4 : mi->vector_bits / 3;
+    int ab = mi->enc == ENC_COMBINED ? cb : (mi->enc == ENC_SEPARATE ? mi->scalar_bits : 0);
+    int ep[3][2][4];
+    for (int c = 0; c < 3; ++c)
+        for (int s = 0; s < ns; ++s)
+            for (int e = 0; e < 2; ++e) ep[s][e][c] = (int)get_bits(blk, &pos, cb);
+    for (int s = 0; s < ns; ++s)
+        for (int e = 0; e < 2; ++e) ep[s][e][3] = ab ? (int)get_bits(blk, &pos, ab) : 255;
+    int pbits[3][2] = {{0, 0}, {0, 0}, {0, 0}};
+    if (mi->pbit == 2)
+        for (int s = 0; s < ns; ++s) {
+            pbits[s][0] = (int)get_bits(blk, &pos, 1);
+            pbits[s][1] = (int)get_bits(blk, &pos, 1);
+        }
+    else if (mi->pbit == 1)
+        for (int s = 0; s < ns; ++s) pbits[s][0] = pbits[s][1] = (int)get_bits(blk, &pos, 1);
+    for (int s = 0; s < ns; ++s)
+        for (int e = 0; e < 2; ++e)
+            for (int c = 0; c < 4; ++c) {
+                int bits = c < 3 ? cb : ab;
+                if (!bits) continue;
+                int v = ep[s][e][c];
+                if (mi->pbit) {
+                    v = (v << 1) | pbits[s][e];
+                    bits++;
+                }
+                v <<= (8 - bits);
+                ep[s][e][c] = v | (v >> bits);
+            }
+    int i0[16], i1[16];
+    const int ib0 = mi->ib0, ib1 = mi->ib1;
+    for (int i = 0; i < 16; ++i) {
+        const int s = (int)shape_of(ns, part, i);
+        const int anchor = i == anchor_of(ns, part, s);
+        i0[i] = (int)get_bits(blk, &pos, anchor ? ib0 - 1 : ib0);
+    }
+    if (ib1)
+        for (int i = 0; i < 16; ++i) i1[i] = (int)get_bits(blk, &pos, i == 0 ? ib1 - 1 : ib1);
+    for (int i = 0; i < 16; ++i) {
+        const int s = (int)shape_of(ns, part, i);
+        int ci, ai, cbits, abits;
+        if (ib1) {
+            ci = sel ? i1[i] : i0[i];
+            ai = sel ? i0[i] : i1[i];
+            cbits = sel ? ib1 : ib0;
+            abits = sel ? ib0 : ib1;
+        } else {
+            ci = ai = i0[i];
+            cbits = abits = ib0;
+        }
+        const int *wc = cbits == 2 ? w2 : cbits == 3 ? w3 : w4;
+        const int *wa = abits == 2 ? w2 : abits == 3 ? w3 : w4;
+        int px[4];
+        for (int c = 0; c < 3; ++c)
+            px[c] = ((64 - wc[ci]) * ep[s][0][c] + wc[ci] * ep[s][1][c] + 32) >> 6;
+        px[3] = ((64 - wa[ai]) * ep[s][0][3] + wa[ai] * ep[s][1][3] + 32) >> 6;
+        if (rot == 1) { int t = px[0]; px[0] = px[3]; px[3] = t; }
+        else if (rot == 2) { int t = px[1]; px[1] = px[3]; px[3] = t; }
+        else if (rot == 3) { int t = px[2]; px[2] = px[3]; px[3] = t; }
+        for (int c = 0; c < 4; ++c) rgba[i * 4 + c] = (uint8_t)px[c];
+    }
+}

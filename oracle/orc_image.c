@@ -1,0 +1,150 @@
+/*
+ * orc_image.c -- image-level drivers for the CPU restatement.
+ *
+ * TEST INFRASTRUCTURE ONLY (see bcn_oracle.h).  Restates the block loops of
+ * src/amd_bc{1,4,5,7}_compressor.cpp (raster order over slices, block rows,
+ * block columns) and ReadNxNBlockF / ReadNxNSingleBlockF edge clamping
+ * (src/block_utils.cpp:7-41, :116-144).  The UNORM8 -> float conversion
+ * (Image_GetPixelAtF in the un-vendored gfx_image) is restated as v/255.0f.
+ * A pthread pool over block rows provides the multi-core CPU baseline.
+ */
+#include "bcn_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+uint64_t orc_fnv1a64(const uint8_t *p, size_t n)
+{
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (size_t i = 0; i < n; ++i) {
+        h ^= p[i];
+        h *= 0x100000001b3ull;
+    }
+    return h;
+}
+
+static float unorm8(uint8_t v) { return (float)v / 255.0f; }
+
+/* ReadNxNBlockF, block_utils.cpp:7-41: x/y beyond the image clamp to the
+ * last column/row.  Missing channels read as 0 (alpha as 1). */
+void orc_load_block_rgba8(const uint8_t *src, uint32_t width, uint32_t height, uint32_t channels,
+                          uint32_t bx, uint32_t by, int force_alpha_one, float out[64])
+{
+    for (uint32_t y = 0; y < 4; ++y) {
+        uint32_t sy = by * 4 + y;
+        if (sy >= height) sy = height - 1;
+        for (uint32_t x = 0; x < 4; ++x) {
+            uint32_t sx = bx * 4 + x;
+            if (sx >= width) sx = width - 1;
+            const uint8_t *p = src + ((size_t)sy * width + sx) * channels;
+            float *o = out + (y * 4 + x) * 4;
+            o[0] = unorm8(p[0]);
+            o[1] = channels > 1 ? unorm8(p[1]) : 0.f;
+            o[2] = channels > 2 ? unorm8(p[2]) : 0.f;
+            o[3] = channels > 3 ? unorm8(p[3]) : 1.f;
+            if (force_alpha_one) o[3] = 1.0f;
+        }
+    }
+}
+
+typedef struct {
+    int fmt;
+    const uint8_t *src;
+    uint32_t width, height, slices, channels;
+    int bc4_channel;
+    uint32_t row0, nrows, bx_count, by_count;
+    uint8_t *dst;
+    double *err;
+    int next;            /* next job (slice*nrows + row) */
+    int njobs;
+    pthread_mutex_t lock;
+} job_t;
+
+static size_t block_bytes(int fmt) { return (fmt == 1 || fmt == 4) ? 8 : 16; }
+
+static void encode_row(job_t *j, uint32_t slice, uint32_t brow)
+{
+    const size_t slice_px = (size_t)j->width * j->height * j->channels;
+    const uint8_t *img = j->src + slice_px * slice;
+    const size_t bb = block_bytes(j->fmt);
+    const int has_alpha = j->channels > 3;
+    /* output is the shard's own contiguous region: rows [row0,row0+nrows) of every slice */
+    const size_t out_row = ((size_t)slice * j->nrows + (brow - j->row0)) * j->bx_count;
+    for (uint32_t bx = 0; bx < j->bx_count; ++bx) {
+        float blk[64], ch[16];
+        uint8_t *o = j->dst + (out_row + bx) * bb;
+        double e = 0.0;
+        orc_load_block_rgba8(img, j->width, j->height, j->channels, bx, brow, !has_alpha, blk);
+        switch (j->fmt) {
+        case 1:
+            /* Image_CompressAMDBC1 defaults: steps 1, threshold 128/255 */
+            orc_bc1_block(blk, 1, 128 / 255.0f, o);
+            break;
+        case 4:
+            for (int i = 0; i < 16; ++i) ch[i] = blk[i * 4 + j->bc4_channel];
+            orc_bc4_block(ch, o);
+            break;
+        case 5:
+            for (int i = 0; i < 16; ++i) ch[i] = blk[i * 4 + 0];
+            orc_bc4_block(ch, o);
+            for (int i = 0; i < 16; ++i) ch[i] = blk[i * 4 + 1];
+            orc_bc4_block(ch, o + 8);
+            break;
+        case 7:
+            /* Image_CompressAMDBC7 (amd_bc7_compressor.cpp:58-65) */
+            e = orc_bc7_block(blk, 0xFF, has_alpha, 1.0f, 1, 1, 1.0f, o);
+            break;
+        }
+        if (j->err) j->err[out_row + bx] = e;
+    }
+}
+
+static void *worker(void *arg)
+{
+    job_t *j = (job_t *)arg;
+    for (;;) {
+        pthread_mutex_lock(&j->lock);
+        int k = j->next++;
+        pthread_mutex_unlock(&j->lock);
+        if (k >= j->njobs) break;
+        encode_row(j, (uint32_t)(k / (int)j->nrows), j->row0 + (uint32_t)(k % (int)j->nrows));
+    }
+    return NULL;
+}
+
+int orc_encode_image(int fmt, const uint8_t *src, uint32_t width, uint32_t height, uint32_t slices,
+                     uint32_t channels, int bc4_channel, int32_t first_row, int32_t num_rows,
+                     int threads, uint8_t *dst, double *block_err)
+{
+    if (!src || !dst || !width || !height || !slices || channels < 1 || channels > 4) return -1;
+    if (fmt != 1 && fmt != 4 && fmt != 5 && fmt != 7) return -1;
+    job_t j;
+    memset(&j, 0, sizeof(j));
+    j.fmt = fmt;
+    j.src = src;
+    j.width = width;
+    j.height = height;
+    j.slices = slices;
+    j.channels = channels;
+    j.bc4_channel = bc4_channel;
+    j.bx_count = (width + 3) / 4;
+    j.by_count = (height + 3) / 4;
+    j.row0 = first_row < 0 ? 0 : (uint32_t)first_row;
+    j.nrows = num_rows < 0 ? j.by_count - j.row0 : (uint32_t)num_rows;
+    if (j.row0 + j.nrows > j.by_count) return -1;
+    j.dst = dst;
+    j.err = block_err;
+    j.njobs = (int)(j.nrows * slices);
+    pthread_mutex_init(&j.lock, NULL);
+    if (threads <= 1) {
+        worker(&j);
+    } else {
+        pthread_t *t = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)threads);
+        for (int i = 0; i < threads; ++i) pthread_create(&t[i], NULL, worker, &j);
+        for (int i = 0; i < threads; ++i) pthread_join(t[i], NULL);
+        free(t);
+    }
+    pthread_mutex_destroy(&j.lock);
+    return 0;
+}
