@@ -1,0 +1,218 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X BCn block-compression hot path.
+
+Metric (BASELINE.json): Mpixels/s (and blocks/s) BC1 & BC7 on 8K RGBA8.
+Default workload = configs[1]: BC1 default quality on an 8192x8192 synthetic
+RGBA8 texture (G1: gradient + noise), inputs resident in HBM, one rank per
+GPU.  With N ranks the job is an (8192*N) x 8192 texture sharded by block
+rows, each rank encoding its own 8192-row shard (weak scaling, no collective
+in the timed region; the optional RCCL gather of the packed bitstream is
+timed separately with --gather).
+
+A "step" = one launch of the encoder over the rank's whole shard.  value =
+pixels of all ranks x steps / max-over-ranks wall time.  roofline: the
+encoder kernel's algorithmic bytes (72 B/block BC1, 80 B/block
+BC7, 24 B/block BC4, 48 B/block BC5) per launch / its average duration,
+measured with HIP events on the launch stream, against 8 TB/s.  cpu_baseline:
+the CPU restatement (oracle/, test infrastructure) timed on a bounded sample
+of block rows of the same texture on the host cores (rank 0 only); the GPU
+output of those rows is checked bit-for-bit against it.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FMTS = {"bc1": 1, "bc4": 4, "bc5": 5, "bc7": 7}
+ALG_BYTES = {1: 72, 4: 24, 5: 48, 7: 80}   # source texels read + block written
+CHANNELS = {1: 4, 4: 1, 5: 2, 7: 4}
+HBM_PEAK_GBS = 8000.0                        # MI355X_MICROARCH.md chip table (spec)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--format", default="bc1", choices=sorted(FMTS))
+    p.add_argument("--size", type=int, default=8192, help="texture width = rows per rank")
+    p.add_argument("--rows", type=int, default=0, help="BC7: block rows per rank (0 = all)")
+    p.add_argument("--gather", action="store_true", help="time an RCCL gather of the bitstream to rank 0")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--traffic-json", default="")
+    return p.parse_args()
+
+
+def make_source(fmt, size, rank, device):
+    import torch
+    from gfx_imagecompress_amd import synth
+    if fmt in (1, 7):
+        return synth.g1_torch(size, size, 1, seed=0x9E3779B9 + rank, device=device)
+    import numpy as np
+    h = synth.height_field(size, size, seed=1 + rank)
+    if fmt == 4:
+        return torch.from_numpy(h[None, :, :, None].copy()).to(device)
+    return torch.from_numpy(synth.normal_map(h)[None].copy()).to(device)
+
+
+def cpu_baseline(fmt, src_host, size, gpu_blocks, budget_s):
+    """Oracle on a bounded prefix of block rows; returns (dict, parity_ok)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, os.cpu_count() or 1, 64))
+    bx = (size + 3) // 4
+    by = (size + 3) // 4
+    rows = 2 if fmt == 7 else 16
+    t0 = time.perf_counter()
+    out = oracle_lib.encode_image(fmt, src_host, bc4_channel=0, first_row=0, num_rows=rows, threads=threads)
+    dt = time.perf_counter() - t0
+    # grow the sample to ~budget_s of CPU work (bounded by the image)
+    if dt < budget_s / 4 and rows < by:
+        more = int(min(by, max(rows, rows * (budget_s / max(dt, 1e-3)))))
+        more = max(rows, min(by, more))
+        if more > rows:
+            rows = more
+            t0 = time.perf_counter()
+            out = oracle_lib.encode_image(fmt, src_host, bc4_channel=0, first_row=0, num_rows=rows, threads=threads)
+            dt = time.perf_counter() - t0
+    px = rows * 4 * size
+    gpu_rows = gpu_blocks.reshape(by, bx, -1)[:rows].reshape(out.shape)
+    parity = bool(np.array_equal(gpu_rows, out))
+    mism = int((gpu_rows != out).any(axis=1).sum())
+    res = {"value": round(px / dt / 1e6, 4), "unit": "Mpixels/s", "cores": threads, "kind": "port",
+           "sample": f"block rows 0-{rows - 1} of rank 0's {size}x{size} texture ({rows * bx} blocks, "
+                     f"{dt:.1f} s, {threads} threads)",
+           "blocks_per_s": round(rows * bx / dt, 1)}
+    return res, parity, mism
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import gfx_imagecompress_amd as gic
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    fmt = FMTS[args.format]
+    size = args.size
+    bx, by = (size + 3) // 4, (size + 3) // 4
+    rows = by if not args.rows else min(args.rows, by)
+    src = make_source(fmt, size, rank, dev)
+    ch = CHANNELS[fmt]
+    nblocks = bx * rows
+    dst = torch.empty(nblocks * gic.block_bytes(fmt), dtype=torch.uint8, device=dev)
+    opts = gic.Options(bc4_channel=0)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        gic.encode_device(fmt, src, size, size, 1, ch, dst, opts, 0, rows, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall, kern_ms = float(t[0]), float(t[1])
+
+    gather_ms = None
+    if args.gather and world > 1:
+        out_all = torch.empty(world * dst.numel(), dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        g0 = time.perf_counter()
+        dist.all_gather_into_tensor(out_all, dst)
+        torch.cuda.synchronize(dev)
+        gather_ms = (time.perf_counter() - g0) * 1e3
+
+    pixels = size * rows * 4 * world          # pixels encoded per step, all ranks
+    value = pixels * args.steps / wall / 1e6
+    alg_bytes = ALG_BYTES[fmt] * nblocks      # per launch, per rank
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    tj = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{args.format}.json")
+    if os.path.exists(tj):
+        try:
+            with open(tj) as f:
+                tr = json.load(f)
+            if tr.get("size") == size and tr.get("rows") == rows:
+                traffic = tr.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    cpu = None
+    parity = None
+    if rank == 0 and not args.no_cpu:
+        host = src.cpu().numpy()[0]
+        torch.cuda.synchronize(dev)
+        cpu, parity, mism = cpu_baseline(fmt, host, size, dst.cpu().numpy(), args.cpu_seconds)
+        cpu["gpu_parity"] = "bit-exact" if parity else f"{mism} blocks differ"
+
+    if rank == 0:
+        line = {
+            "metric": "Mpixels/s (and blocks/s) BC1 & BC7 on 8K RGBA8 at 1/2/4/8 MI355X",
+            "value": round(value, 3),
+            "unit": "Mpixels/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32" if fmt != 7 else "f64",
+            "data": "synthetic",
+            "config": {"workload": f"{args.format.upper()} default quality, {size}x{size * world} synthetic "
+                                   f"{'RGBA8 G1 gradient+noise' if fmt in (1, 7) else ('R8 height' if fmt == 4 else 'RG8 normal')}"
+                                   f", block-row shards of {size}x{rows * 4} per GPU",
+                       "format": args.format.upper(), "width": size, "rows_per_gpu": rows * 4,
+                       "global_batch_blocks": nblocks * world, "parallelism": f"block-row shards x{world}"},
+            "blocks_per_s": round(nblocks * world * args.steps / wall, 1),
+            "kernel_ms": round(kern_ms, 4),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+                         "alg_bytes_per_launch": alg_bytes,
+                         "note": "compute (VALU) bound; HBM fraction reported per BASELINE.json"},
+            "cpu_baseline": cpu,
+        }
+        if gather_ms is not None:
+            line["gather_ms"] = round(gather_ms, 3)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,238 @@
+"""gfx_imagecompress_amd -- MI355X-native BCn block compressor.
+
+Python mirror of the reference's ``Image_Compress*`` operator interface
+(DeanoC/gfx_imagecompress ``include/gfx_imagecompress/imagecompress.h``) over
+the C ABI of ``lib/libgfx_imagecompress_amd.so`` (HIP kernels for gfx950).
+
+* :func:`encode_device` -- the batched device entry (``gic_hip_encode_rows``):
+  inputs already resident in HBM (torch tensors), asynchronous on a stream.
+* :func:`compress_bc1` / :func:`compress_bc4` / :func:`compress_bc5` /
+  :func:`compress_bc7` -- host-array convenience wrappers with the reference
+  wrappers' defaults (``amd_bc{1,4,5,7}_compressor.cpp``).
+
+There is no CPU fallback: if the shared library or a GPU is missing every
+compression call raises :class:`GicError`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+__all__ = [
+    "GicError", "Options", "FMT_BC1", "FMT_BC4", "FMT_BC5", "FMT_BC7", "library",
+    "block_bytes", "blocks_shape", "encode_device", "encode_blocks_f32", "compress_bc1",
+    "compress_bc4", "compress_bc5", "compress_bc7", "LIB_PATH",
+]
+
+FMT_BC1, FMT_BC4, FMT_BC5, FMT_BC7 = 1, 4, 5, 7
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libgfx_imagecompress_amd.so")
+
+GIC_OK, GIC_EINVAL, GIC_EUNSUP, GIC_EHIP = 0, -1, -2, -3
+_ERRS = {GIC_EINVAL: "invalid argument", GIC_EUNSUP: "unsupported option", GIC_EHIP: "HIP runtime error"}
+
+
+class GicError(RuntimeError):
+    """Raised when the HIP library is missing or a call fails."""
+
+
+class _COptions(ctypes.Structure):
+    _fields_ = [
+        ("struct_size", ctypes.c_uint32),
+        ("bc1_alpha_threshold", ctypes.c_float),
+        ("refinement_steps", ctypes.c_uint8),
+        ("b3d_refinement", ctypes.c_uint8),
+        ("adaptive_weights", ctypes.c_uint8),
+        ("bc4_channel", ctypes.c_uint8),
+        ("bc7_mode_mask", ctypes.c_uint8),
+        ("colour_restrict", ctypes.c_uint8),
+        ("alpha_restrict", ctypes.c_uint8),
+        ("force_alpha_one", ctypes.c_uint8),
+        ("bc7_quality", ctypes.c_float),
+        ("bc7_performance", ctypes.c_float),
+    ]
+
+
+@dataclass
+class Options:
+    """Mirror of ``gic_options`` with the reference defaults.
+
+    bc1_alpha_threshold: ``Image_CompressBC1Options.AlphaThreshold / 255``
+    (amd_bc1_compressor.cpp:57; alpha-aware even when UseAlpha is false).
+    refinement_steps: ``Image_CompressAMDBackendOptions.RefinementSteps``.
+    bc4_channel: the reference BC4 wrapper reads channel 1 (green).
+    """
+
+    bc1_alpha_threshold: float = 128 / 255.0
+    refinement_steps: int = 1
+    b3d_refinement: bool = False
+    adaptive_weights: bool = False
+    bc4_channel: int = 1
+    bc7_mode_mask: int = 0xFF
+    colour_restrict: bool = True
+    alpha_restrict: bool = True
+    force_alpha_one: bool = False
+    bc7_quality: float = 1.0
+    bc7_performance: float = 1.0
+
+    def to_c(self) -> _COptions:
+        o = _COptions()
+        o.struct_size = ctypes.sizeof(_COptions)
+        o.bc1_alpha_threshold = float(self.bc1_alpha_threshold)
+        o.refinement_steps = int(self.refinement_steps)
+        o.b3d_refinement = int(bool(self.b3d_refinement))
+        o.adaptive_weights = int(bool(self.adaptive_weights))
+        o.bc4_channel = int(self.bc4_channel)
+        o.bc7_mode_mask = int(self.bc7_mode_mask)
+        o.colour_restrict = int(bool(self.colour_restrict))
+        o.alpha_restrict = int(bool(self.alpha_restrict))
+        o.force_alpha_one = int(bool(self.force_alpha_one))
+        o.bc7_quality = float(self.bc7_quality)
+        o.bc7_performance = float(self.bc7_performance)
+        return o
+
+
+_lib = None
+
+
+def library() -> ctypes.CDLL:
+    """Load the HIP shared library (raises GicError if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise GicError(f"{LIB_PATH} missing: run `make -C gfx_imagecompress_amd` "
+                       "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, u32, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_size_t
+    lib.gic_hip_encode_rows.argtypes = [ctypes.c_int, vp, u32, u32, u32, u32, sz, u32, u32,
+                                        ctypes.POINTER(_COptions), vp, vp, vp]
+    lib.gic_hip_encode_rows.restype = ctypes.c_int
+    lib.gic_hip_encode.argtypes = [ctypes.c_int, vp, u32, u32, u32, u32, sz,
+                                   ctypes.POINTER(_COptions), vp, vp, vp]
+    lib.gic_hip_encode.restype = ctypes.c_int
+    lib.gic_hip_encode_blocks_f32.argtypes = [ctypes.c_int, vp, u32, ctypes.POINTER(_COptions), vp, vp, vp]
+    lib.gic_hip_encode_blocks_f32.restype = ctypes.c_int
+    lib.gic_default_options.argtypes = [ctypes.POINTER(_COptions)]
+    lib.gic_default_options.restype = None
+    lib.gic_block_bytes.argtypes = [ctypes.c_int]
+    lib.gic_block_bytes.restype = u32
+    lib.gic_last_hip_error.restype = ctypes.c_int
+    lib.gic_version.restype = ctypes.c_char_p
+    _lib = lib
+    return lib
+
+
+def _check(rc: int) -> None:
+    if rc != GIC_OK:
+        extra = ""
+        if rc == GIC_EHIP:
+            extra = f" (hipError {library().gic_last_hip_error()})"
+        raise GicError(f"gic call failed: {_ERRS.get(rc, rc)}{extra}")
+
+
+def block_bytes(fmt: int) -> int:
+    return 8 if fmt in (FMT_BC1, FMT_BC4) else 16
+
+
+def blocks_shape(width: int, height: int) -> tuple[int, int]:
+    """(block columns, block rows) of an image, edge blocks included."""
+    return (width + 3) // 4, (height + 3) // 4
+
+
+def _stream_handle(stream) -> int | None:
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+def encode_device(fmt: int, src, width: int, height: int, slices: int, channels: int, dst,
+                  options: Options | None = None, first_block_row: int = 0,
+                  num_block_rows: int | None = None, block_err=None, stream=None,
+                  row_pitch: int | None = None) -> None:
+    """Asynchronously encode an 8-bit image stack resident in HBM.
+
+    src: uint8 CUDA tensor holding ``slices*height`` rows of ``row_pitch`` bytes.
+    dst: uint8 CUDA tensor receiving ``bx*num_block_rows*slices`` blocks.
+    Launched on ``stream`` (default: torch's current stream).
+    """
+    import torch
+    if not (src.is_cuda and dst.is_cuda):
+        raise GicError("encode_device needs device (HBM) tensors; there is no CPU path")
+    bx, by = blocks_shape(width, height)
+    nrows = by - first_block_row if num_block_rows is None else num_block_rows
+    pitch = width * channels if row_pitch is None else row_pitch
+    need = bx * nrows * slices * block_bytes(fmt)
+    if dst.numel() * dst.element_size() < need:
+        raise GicError(f"dst too small: {dst.numel() * dst.element_size()} < {need}")
+    if src.numel() * src.element_size() < pitch * height * slices:
+        raise GicError("src too small for the given shape")
+    if block_err is not None and (block_err.dtype != torch.float64 or block_err.numel() < bx * nrows * slices):
+        raise GicError("block_err must be float64 with one entry per block")
+    opts = (options or Options()).to_c()
+    rc = library().gic_hip_encode_rows(fmt, src.data_ptr(), width, height, slices, channels, pitch,
+                                       first_block_row, nrows, ctypes.byref(opts), dst.data_ptr(),
+                                       block_err.data_ptr() if block_err is not None else None,
+                                       _stream_handle(stream))
+    _check(rc)
+
+
+def encode_blocks_f32(fmt: int, blocks, dst, options: Options | None = None, block_err=None, stream=None) -> None:
+    """Block-level batch: blocks is a float32 CUDA tensor (n,64) for BC1/BC7 or (n,16) for BC4."""
+    n = blocks.shape[0]
+    opts = (options or Options()).to_c()
+    rc = library().gic_hip_encode_blocks_f32(fmt, blocks.data_ptr(), n, ctypes.byref(opts), dst.data_ptr(),
+                                             block_err.data_ptr() if block_err is not None else None,
+                                             _stream_handle(stream))
+    _check(rc)
+
+
+def _host_compress(fmt: int, image, options: Options):
+    """numpy (H,W,C) or (S,H,W,C) uint8 -> numpy uint8 blocks (S,by,bx,bytes)."""
+    import numpy as np
+    import torch
+    a = np.ascontiguousarray(image)
+    if a.dtype != np.uint8:
+        raise GicError("8-bit sources only")
+    if a.ndim == 2:
+        a = a[:, :, None]
+    if a.ndim == 3:
+        a = a[None]
+    s, h, w, c = a.shape
+    bx, by = blocks_shape(w, h)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    src = torch.from_numpy(a).to(dev)
+    dst = torch.empty(bx * by * s * block_bytes(fmt), dtype=torch.uint8, device=dev)
+    encode_device(fmt, src, w, h, s, c, dst, options)
+    torch.cuda.synchronize()
+    return dst.cpu().numpy().reshape(s, by, bx, block_bytes(fmt))
+
+
+def compress_bc1(image, options: Options | None = None):
+    """Image_CompressAMDBC1 (amd_bc1_compressor.cpp:11-71) on a host array."""
+    o = options or Options()
+    if image.ndim >= 3 and image.shape[-1] < 4:
+        o.force_alpha_one = True
+    return _host_compress(FMT_BC1, image, o)
+
+
+def compress_bc4(image, options: Options | None = None):
+    """Image_CompressAMDBC4 (amd_bc4_compressor.cpp:11-50): channel 1 by default."""
+    return _host_compress(FMT_BC4, image, options or Options())
+
+
+def compress_bc5(image, options: Options | None = None):
+    """Image_CompressAMDBC5 (amd_bc5_compressor.cpp:11-56)."""
+    return _host_compress(FMT_BC5, image, options or Options())
+
+
+def compress_bc7(image, options: Options | None = None):
+    """Image_CompressAMDBC7 (amd_bc7_compressor.cpp:25-81)."""
+    o = options or Options()
+    if image.ndim >= 3 and image.shape[-1] < 4:
+        o.force_alpha_one = True
+    return _host_compress(FMT_BC7, image, o)

@@ -1,0 +1,586 @@
+// gic_api.cpp -- the C ABI of libgfx_imagecompress_amd.so.
+//
+// Two layers:
+//   * gic_hip_* (include/gfx_imagecompress_amd/gic.h): batched, asynchronous
+//     device entry points over images or float blocks resident in HBM.
+//   * Image_Compress* (include/gfx_imagecompress/imagecompress.h): the
+//     reference's host API (include/gfx_imagecompress/imagecompress.h:1-141),
+//     implemented on top of gic_hip_* -- host image in, host image out, with
+//     the reference's option defaults, destination-format choice, block-row
+//     progress callback and NULL-on-failure contract.
+// Every compression call runs the HIP kernels; there is no CPU fallback.
+
+#include <hip/hip_runtime.h>
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <vector>
+
+#include "../../include/gfx_imagecompress/imagecompress.h"
+#include "../../include/gfx_imagecompress_amd/gic.h"
+#include "gic_common.h"
+
+namespace gic {
+hipError_t launch_bc1_image(const Geometry &g, float thr, int steps, int force_alpha_one, void *dst, hipStream_t s);
+hipError_t launch_bc45_image(const Geometry &g, int fmt, int channel, void *dst, hipStream_t s);
+hipError_t launch_bc1_blocks(const float *blocks, uint32_t n, float thr, int steps, void *dst, hipStream_t s);
+hipError_t launch_bc4_blocks(const float *blocks, uint32_t n, void *dst, hipStream_t s);
+hipError_t launch_bc7_image(const Geometry &g, const gic_options &o, void *dst, double *err, hipStream_t s);
+hipError_t launch_bc7_blocks(const float *blocks, uint32_t n, const gic_options &o, void *dst, double *err,
+                             hipStream_t s);
+}  // namespace gic
+
+static thread_local int t_last_hip_error = 0;
+
+static int hip_fail(hipError_t e)
+{
+    t_last_hip_error = (int)e;
+    fprintf(stderr, "gfx_imagecompress_amd: HIP error %d (%s)\n", (int)e, hipGetErrorString(e));
+    return GIC_EHIP;
+}
+
+extern "C" int gic_last_hip_error(void) { return t_last_hip_error; }
+
+extern "C" const char *gic_version(void) { return "gfx_imagecompress_amd 0.1 (gfx950)"; }
+
+extern "C" void gic_default_options(gic_options *o)
+{
+    if (!o) return;
+    memset(o, 0, sizeof(*o));
+    o->struct_size = sizeof(gic_options);
+    o->bc1_alpha_threshold = 128 / 255.0f;   // amd_bc1_compressor.cpp:21-27,57
+    o->refinement_steps = 1;                 // amd_bcx_helpers.cpp:23-31
+    o->bc4_channel = 1;                      // amd_bc4_compressor.cpp:34
+    o->bc7_mode_mask = 0xFF;
+    o->colour_restrict = 1;                  // amd_bc7_compressor.cpp:58-65
+    o->alpha_restrict = 1;
+    o->bc7_quality = 1.0f;
+    o->bc7_performance = 1.0f;
+}
+
+extern "C" uint32_t gic_block_bytes(gic_format fmt)
+{
+    return (fmt == GIC_FMT_BC1 || fmt == GIC_FMT_BC4) ? 8u : 16u;
+}
+
+static int check_options(gic_format fmt, const gic_options &o)
+{
+    if (o.b3d_refinement || o.adaptive_weights) return GIC_EUNSUP;
+    if (o.refinement_steps > 8) return GIC_EINVAL;
+    if (fmt == GIC_FMT_BC4 && o.bc4_channel > 3) return GIC_EINVAL;
+    if (fmt == GIC_FMT_BC7 && (o.bc7_quality != 1.0f || o.bc7_performance != 1.0f)) return GIC_EUNSUP;
+    return GIC_OK;
+}
+
+static bool valid_fmt(gic_format f)
+{
+    return f == GIC_FMT_BC1 || f == GIC_FMT_BC4 || f == GIC_FMT_BC5 || f == GIC_FMT_BC7;
+}
+
+extern "C" int gic_hip_encode_rows(gic_format fmt, const uint8_t *d_src, uint32_t width, uint32_t height,
+                                   uint32_t slices, uint32_t channels, size_t row_pitch, uint32_t first_block_row,
+                                   uint32_t num_block_rows, const gic_options *opt, uint8_t *d_dst,
+                                   double *d_block_err, void *stream)
+{
+    if (!valid_fmt(fmt) || !d_src || !d_dst || !width || !height || !slices || channels < 1 || channels > 4)
+        return GIC_EINVAL;
+    if (row_pitch < (size_t)width * channels) return GIC_EINVAL;
+    const uint32_t by_count = (height + 3) / 4;
+    if (first_block_row >= by_count || num_block_rows == 0 || first_block_row + num_block_rows > by_count)
+        return GIC_EINVAL;
+    gic_options o;
+    gic_default_options(&o);
+    if (opt) {
+        if (opt->struct_size != sizeof(gic_options)) return GIC_EINVAL;
+        o = *opt;
+    }
+    int rc = check_options(fmt, o);
+    if (rc) return rc;
+    const uint64_t total = (uint64_t)((width + 3) / 4) * num_block_rows * slices;
+    if (total > 0xffffffffull) return GIC_EINVAL;
+    gic::Geometry g;
+    g.src = d_src;
+    g.width = width;
+    g.height = height;
+    g.slices = slices;
+    g.channels = channels;
+    g.row_pitch = row_pitch;
+    g.bx_count = (width + 3) / 4;
+    g.row0 = first_block_row;
+    g.nrows = num_block_rows;
+    g.total = (uint32_t)total;
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e = hipSuccess;
+    if (d_block_err && fmt != GIC_FMT_BC7) {
+        e = hipMemsetAsync(d_block_err, 0, sizeof(double) * total, s);
+        if (e != hipSuccess) return hip_fail(e);
+    }
+    switch (fmt) {
+    case GIC_FMT_BC1:
+        e = gic::launch_bc1_image(g, o.bc1_alpha_threshold, o.refinement_steps, o.force_alpha_one, d_dst, s);
+        break;
+    case GIC_FMT_BC4:
+    case GIC_FMT_BC5:
+        e = gic::launch_bc45_image(g, (int)fmt, o.bc4_channel, d_dst, s);
+        break;
+    case GIC_FMT_BC7:
+        e = gic::launch_bc7_image(g, o, d_dst, d_block_err, s);
+        break;
+    }
+    if (e != hipSuccess) return hip_fail(e);
+    return GIC_OK;
+}
+
+extern "C" int gic_hip_encode(gic_format fmt, const uint8_t *d_src, uint32_t width, uint32_t height,
+                              uint32_t slices, uint32_t channels, size_t row_pitch, const gic_options *opt,
+                              uint8_t *d_dst, double *d_block_err, void *stream)
+{
+    if (!height) return GIC_EINVAL;
+    return gic_hip_encode_rows(fmt, d_src, width, height, slices, channels, row_pitch, 0, (height + 3) / 4, opt,
+                               d_dst, d_block_err, stream);
+}
+
+extern "C" int gic_hip_encode_blocks_f32(gic_format fmt, const float *d_blocks, uint32_t n, const gic_options *opt,
+                                         uint8_t *d_dst, double *d_block_err, void *stream)
+{
+    if (!d_blocks || !d_dst || !n) return GIC_EINVAL;
+    if (fmt != GIC_FMT_BC1 && fmt != GIC_FMT_BC4 && fmt != GIC_FMT_BC7) return GIC_EINVAL;
+    gic_options o;
+    gic_default_options(&o);
+    if (opt) {
+        if (opt->struct_size != sizeof(gic_options)) return GIC_EINVAL;
+        o = *opt;
+    }
+    int rc = check_options(fmt, o);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e = hipSuccess;
+    if (fmt == GIC_FMT_BC1)
+        e = gic::launch_bc1_blocks(d_blocks, n, o.bc1_alpha_threshold, o.refinement_steps, d_dst, s);
+    else if (fmt == GIC_FMT_BC4)
+        e = gic::launch_bc4_blocks(d_blocks, n, d_dst, s);
+    else
+        e = gic::launch_bc7_blocks(d_blocks, n, o, d_dst, d_block_err, s);
+    if (e != hipSuccess) return hip_fail(e);
+    return GIC_OK;
+}
+
+// ------------------------------------------------------------------------
+// Image model (stand-in for the un-vendored gfx_image, see gfx_image/image.h)
+// ------------------------------------------------------------------------
+
+extern "C" uint32_t TinyImageFormat_ChannelCount(TinyImageFormat f)
+{
+    switch (f) {
+    case TinyImageFormat_R8_UNORM:
+    case TinyImageFormat_R8_SNORM:
+    case TinyImageFormat_DXBC4_UNORM:
+    case TinyImageFormat_DXBC4_SNORM: return 1;
+    case TinyImageFormat_R8G8_UNORM:
+    case TinyImageFormat_R8G8_SNORM:
+    case TinyImageFormat_DXBC5_UNORM:
+    case TinyImageFormat_DXBC5_SNORM: return 2;
+    case TinyImageFormat_R8G8B8_UNORM:
+    case TinyImageFormat_R8G8B8_SRGB:
+    case TinyImageFormat_DXBC1_RGB_UNORM:
+    case TinyImageFormat_DXBC1_RGB_SRGB: return 3;
+    case TinyImageFormat_R8G8B8A8_UNORM:
+    case TinyImageFormat_R8G8B8A8_SRGB:
+    case TinyImageFormat_R32G32B32A32_SFLOAT:
+    case TinyImageFormat_DXBC1_RGBA_UNORM:
+    case TinyImageFormat_DXBC1_RGBA_SRGB:
+    case TinyImageFormat_DXBC7_UNORM:
+    case TinyImageFormat_DXBC7_SRGB: return 4;
+    default: return 0;
+    }
+}
+
+extern "C" bool TinyImageFormat_IsSRGB(TinyImageFormat f)
+{
+    return f == TinyImageFormat_R8G8B8_SRGB || f == TinyImageFormat_R8G8B8A8_SRGB ||
+           f == TinyImageFormat_DXBC1_RGB_SRGB || f == TinyImageFormat_DXBC1_RGBA_SRGB ||
+           f == TinyImageFormat_DXBC7_SRGB;
+}
+
+extern "C" bool TinyImageFormat_IsSigned(TinyImageFormat f)
+{
+    return f == TinyImageFormat_R8_SNORM || f == TinyImageFormat_R8G8_SNORM || f == TinyImageFormat_DXBC4_SNORM ||
+           f == TinyImageFormat_DXBC5_SNORM || f == TinyImageFormat_R32G32B32A32_SFLOAT;
+}
+
+extern "C" bool TinyImageFormat_IsFloat(TinyImageFormat f) { return f == TinyImageFormat_R32G32B32A32_SFLOAT; }
+
+extern "C" bool TinyImageFormat_IsCompressed(TinyImageFormat f) { return f >= TinyImageFormat_DXBC1_RGB_UNORM; }
+
+extern "C" bool TinyImageFormat_IsNormalised(TinyImageFormat f)
+{
+    return f != TinyImageFormat_UNDEFINED && f != TinyImageFormat_R32G32B32A32_SFLOAT && f < TinyImageFormat_Count;
+}
+
+extern "C" uint32_t TinyImageFormat_BitSizeOfBlock(TinyImageFormat f)
+{
+    if (!TinyImageFormat_IsCompressed(f)) {
+        if (f == TinyImageFormat_R32G32B32A32_SFLOAT) return 128;
+        return 8 * TinyImageFormat_ChannelCount(f);
+    }
+    switch (f) {
+    case TinyImageFormat_DXBC1_RGB_UNORM:
+    case TinyImageFormat_DXBC1_RGB_SRGB:
+    case TinyImageFormat_DXBC1_RGBA_UNORM:
+    case TinyImageFormat_DXBC1_RGBA_SRGB:
+    case TinyImageFormat_DXBC4_UNORM:
+    case TinyImageFormat_DXBC4_SNORM: return 64;
+    default: return 128;
+    }
+}
+
+static uint64_t image_bytes(uint32_t w, uint32_t h, uint32_t d, uint32_t slices, TinyImageFormat f)
+{
+    if (TinyImageFormat_IsCompressed(f))
+        return (uint64_t)((w + 3) / 4) * ((h + 3) / 4) * d * slices * (TinyImageFormat_BitSizeOfBlock(f) / 8);
+    return (uint64_t)w * h * d * slices * (TinyImageFormat_BitSizeOfBlock(f) / 8);
+}
+
+extern "C" Image_ImageHeader const *Image_CreateNoClear(uint32_t w, uint32_t h, uint32_t d, uint32_t slices,
+                                                        TinyImageFormat f)
+{
+    if (!w || !h || !d || !slices || f <= TinyImageFormat_UNDEFINED || f >= TinyImageFormat_Count) return nullptr;
+    Image_ImageHeader *img = (Image_ImageHeader *)calloc(1, sizeof(Image_ImageHeader));
+    if (!img) return nullptr;
+    if (TinyImageFormat_IsCompressed(f)) {
+        w = (w + 3) & ~3u;   // block formats pad to whole blocks
+        h = (h + 3) & ~3u;
+    }
+    img->width = w;
+    img->height = h;
+    img->depth = d;
+    img->slices = slices;
+    img->format = f;
+    img->dataSize = image_bytes(w, h, d, slices, f);
+    img->data = malloc(img->dataSize ? img->dataSize : 1);
+    if (!img->data) {
+        free(img);
+        return nullptr;
+    }
+    return img;
+}
+
+extern "C" Image_ImageHeader const *Image_Create(uint32_t w, uint32_t h, uint32_t d, uint32_t slices,
+                                                 TinyImageFormat f)
+{
+    Image_ImageHeader const *img = Image_CreateNoClear(w, h, d, slices, f);
+    if (img) memset(img->data, 0, img->dataSize);
+    return img;
+}
+
+extern "C" void Image_Destroy(Image_ImageHeader const *img)
+{
+    if (!img) return;
+    free(img->data);
+    free((void *)img);
+}
+
+extern "C" void *Image_RawDataPtr(Image_ImageHeader const *img) { return img ? img->data : nullptr; }
+
+// ------------------------------------------------------------------------
+// Reference host API
+// ------------------------------------------------------------------------
+
+extern "C" void Image_CompressInit(void) {}
+extern "C" void Image_CompressDeinit(void) {}
+
+// Device scratch reused by the synchronous host entry points of one thread.
+struct DeviceScratch {
+    void *src = nullptr, *dst = nullptr;
+    size_t src_bytes = 0, dst_bytes = 0;
+    hipStream_t stream = nullptr;
+    ~DeviceScratch()
+    {
+        if (src) (void)hipFree(src);
+        if (dst) (void)hipFree(dst);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+    bool reserve(size_t sb, size_t db)
+    {
+        if (!stream && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return false;
+        if (sb > src_bytes) {
+            if (src) (void)hipFree(src);
+            src = nullptr;
+            src_bytes = 0;
+            if (hipMalloc(&src, sb) != hipSuccess) return false;
+            src_bytes = sb;
+        }
+        if (db > dst_bytes) {
+            if (dst) (void)hipFree(dst);
+            dst = nullptr;
+            dst_bytes = 0;
+            if (hipMalloc(&dst, db) != hipSuccess) return false;
+            dst_bytes = db;
+        }
+        return true;
+    }
+};
+static thread_local DeviceScratch t_scratch;
+
+// Host-image driver shared by the image-level wrappers: uploads the source,
+// encodes in chunks of block rows, reports progress per block row exactly as
+// the reference loops do (amd_bc1_compressor.cpp:64-68), downloads blocks.
+static Image_ImageHeader const *encode_host_image(Image_ImageHeader const *src, gic_format fmt, TinyImageFormat dst_fmt,
+                                                  const gic_options &o, Image_CompressProgressFunc cb, void *user)
+{
+    if (!src || !src->data || src->depth > 1) return nullptr;
+    const uint32_t ch = TinyImageFormat_ChannelCount(src->format);
+    if (!ch || TinyImageFormat_IsCompressed(src->format) || TinyImageFormat_IsFloat(src->format) ||
+        TinyImageFormat_IsSigned(src->format))
+        return nullptr;   // 8-bit UNORM/sRGB sources only
+    Image_ImageHeader const *dst = Image_CreateNoClear(src->width, src->height, 1, src->slices, dst_fmt);
+    if (!dst) return nullptr;
+    const uint32_t bx = (src->width + 3) / 4, by = (src->height + 3) / 4;
+    const size_t pitch = (size_t)src->width * ch;
+    const size_t src_bytes = pitch * src->height * src->slices;
+    const size_t bb = gic_block_bytes(fmt);
+    const size_t dst_bytes = (size_t)bx * by * src->slices * bb;
+    DeviceScratch &s = t_scratch;
+    bool ok = s.reserve(src_bytes, dst_bytes) &&
+              hipMemcpyAsync(s.src, src->data, src_bytes, hipMemcpyHostToDevice, s.stream) == hipSuccess;
+    const uint32_t chunk = cb ? 16u : by;   // rows per launch when reporting progress
+    for (uint32_t w = 0; ok && w < src->slices; ++w) {
+        const uint8_t *slice_src = (const uint8_t *)s.src + pitch * src->height * w;
+        uint8_t *slice_dst = (uint8_t *)s.dst + (size_t)bx * by * bb * w;
+        for (uint32_t y0 = 0; ok && y0 < by; y0 += chunk) {
+            const uint32_t n = (by - y0) < chunk ? (by - y0) : chunk;
+            ok = gic_hip_encode_rows(fmt, slice_src, src->width, src->height, 1, ch, pitch, y0, n, &o,
+                                     slice_dst + (size_t)y0 * bx * bb, nullptr, s.stream) == GIC_OK;
+            if (ok && cb) {
+                ok = hipStreamSynchronize(s.stream) == hipSuccess;
+                for (uint32_t y = y0; ok && y < y0 + n; ++y) {
+                    const float pct = 100.f * (y * bx) / (bx * by);
+                    if (cb(user, pct)) {   // abort requested
+                        Image_Destroy(dst);
+                        return nullptr;
+                    }
+                }
+            }
+        }
+    }
+    ok = ok && hipMemcpyAsync(dst->data, s.dst, dst_bytes, hipMemcpyDeviceToHost, s.stream) == hipSuccess &&
+         hipStreamSynchronize(s.stream) == hipSuccess;
+    if (!ok) {
+        fprintf(stderr, "gfx_imagecompress_amd: GPU encode failed (HIP error %d)\n", (int)hipGetLastError());
+        Image_Destroy(dst);
+        return nullptr;
+    }
+    return dst;
+}
+
+static Image_CompressAMDBackendOptions const kDefaultAmd = {false, false, 1, 0xFF};   // amd_bcx_helpers.cpp:23-31
+
+extern "C" Image_ImageHeader const *Image_CompressAMDBC1(Image_ImageHeader const *src,
+                                                         Image_CompressAMDBackendOptions const *amd,
+                                                         Image_CompressBC1Options const *options,
+                                                         Image_CompressProgressFunc cb, void *user)
+{
+    static Image_CompressBC1Options const kDefaultBc1 = {false, 128};   // amd_bc1_compressor.cpp:21-27
+    if (!src) return nullptr;
+    amd = amd ? amd : &kDefaultAmd;
+    options = options ? options : &kDefaultBc1;
+    const bool srgb = TinyImageFormat_IsSRGB(src->format);
+    const bool dst_alpha = options->UseAlpha;
+    // amd_bc1_compressor.cpp:33-35 (sRGB without alpha keeps the UNORM RGB format, as the reference does)
+    TinyImageFormat f = srgb ? (dst_alpha ? TinyImageFormat_DXBC1_RGBA_SRGB : TinyImageFormat_DXBC1_RGB_UNORM)
+                             : (dst_alpha ? TinyImageFormat_DXBC1_RGBA_UNORM : TinyImageFormat_DXBC1_RGB_UNORM);
+    gic_options o;
+    gic_default_options(&o);
+    o.b3d_refinement = amd->b3DRefinement;
+    o.adaptive_weights = amd->AdaptiveColourWeights;
+    o.refinement_steps = amd->RefinementSteps;
+    o.bc1_alpha_threshold = options->AlphaThreshold / 255.0f;
+    o.force_alpha_one = TinyImageFormat_ChannelCount(src->format) > 3 ? 0 : 1;
+    return encode_host_image(src, GIC_FMT_BC1, f, o, cb, user);
+}
+
+extern "C" Image_ImageHeader const *Image_CompressAMDBC4(Image_ImageHeader const *src, Image_CompressProgressFunc cb,
+                                                         void *user)
+{
+    if (!src) return nullptr;
+    TinyImageFormat f = TinyImageFormat_IsSigned(src->format) ? TinyImageFormat_DXBC4_SNORM : TinyImageFormat_DXBC4_UNORM;
+    gic_options o;
+    gic_default_options(&o);
+    o.bc4_channel = 1;   // Q1: the reference reads green (amd_bc4_compressor.cpp:34-35)
+    return encode_host_image(src, GIC_FMT_BC4, f, o, cb, user);
+}
+
+extern "C" Image_ImageHeader const *Image_CompressAMDBC5(Image_ImageHeader const *src, Image_CompressProgressFunc cb,
+                                                         void *user)
+{
+    if (!src) return nullptr;
+    TinyImageFormat f = TinyImageFormat_IsSigned(src->format) ? TinyImageFormat_DXBC5_SNORM : TinyImageFormat_DXBC5_UNORM;
+    gic_options o;
+    gic_default_options(&o);
+    return encode_host_image(src, GIC_FMT_BC5, f, o, cb, user);
+}
+
+extern "C" Image_ImageHeader const *Image_CompressAMDBC7(Image_ImageHeader const *src,
+                                                         Image_CompressAMDBackendOptions const *amd,
+                                                         Image_CompressProgressFunc cb, void *user)
+{
+    if (!src) return nullptr;
+    amd = amd ? amd : &kDefaultAmd;
+    TinyImageFormat f = TinyImageFormat_IsSRGB(src->format) ? TinyImageFormat_DXBC7_SRGB : TinyImageFormat_DXBC7_UNORM;
+    gic_options o;
+    gic_default_options(&o);
+    o.bc7_mode_mask = amd->ModeMask;   // amd_bc7_compressor.cpp:58-65
+    o.force_alpha_one = TinyImageFormat_ChannelCount(src->format) > 3 ? 0 : 1;
+    return encode_host_image(src, GIC_FMT_BC7, f, o, cb, user);
+}
+
+// Formats outside this release's hot path (BC2/BC3/BC6H
+// and the bc7enc16 fast path are "next"): exported for link compatibility,
+// they report failure the way the reference reports any failure (NULL).
+extern "C" Image_ImageHeader const *Image_CompressAMDBC2(Image_ImageHeader const *, Image_CompressAMDBackendOptions const *,
+                                                         Image_CompressProgressFunc, void *)
+{
+    return nullptr;
+}
+extern "C" Image_ImageHeader const *Image_CompressAMDBC3(Image_ImageHeader const *, Image_CompressAMDBackendOptions const *,
+                                                         Image_CompressProgressFunc, void *)
+{
+    return nullptr;
+}
+extern "C" Image_ImageHeader const *Image_CompressAMDBC6H(Image_ImageHeader const *, Image_CompressAMDBackendOptions const *,
+                                                          Image_CompressProgressFunc, void *)
+{
+    return nullptr;
+}
+extern "C" Image_ImageHeader const *Image_CompressRichGel999BC7(Image_ImageHeader const *,
+                                                                Image_CompressRichGel999BackendOptions const *,
+                                                                Image_CompressProgressFunc, void *)
+{
+    return nullptr;
+}
+
+// imagecompress.cpp:20-50 (the reference's trailing Deinit is unreachable)
+extern "C" Image_ImageHeader const *ImageCompress_Compress(Image_CompressType type, bool fast,
+                                                            Image_ImageHeader const *src)
+{
+    Image_CompressInit();
+    switch (type) {
+    case Image_CT_None: return src;
+    case Image_CT_DXBC1: return Image_CompressAMDBC1(src, nullptr, nullptr, nullptr, nullptr);
+    case Image_CT_DXBC2: return Image_CompressAMDBC2(src, nullptr, nullptr, nullptr);
+    case Image_CT_DXBC3: return Image_CompressAMDBC3(src, nullptr, nullptr, nullptr);
+    case Image_CT_DXBC4: return Image_CompressAMDBC4(src, nullptr, nullptr);
+    case Image_CT_DXBC5: return Image_CompressAMDBC5(src, nullptr, nullptr);
+    case Image_CT_DXBC6H: return Image_CompressAMDBC6H(src, nullptr, nullptr, nullptr);
+    case Image_CT_DXBC7:
+        return fast ? Image_CompressRichGel999BC7(src, nullptr, nullptr, nullptr)
+                    : Image_CompressAMDBC7(src, nullptr, nullptr, nullptr);
+    default: return nullptr;
+    }
+}
+
+// imagecompress.cpp:52-116
+extern "C" Image_CompressType ImageCompress_PickCompressionType(Image_CompressPickFlags flags,
+                                                                Image_ImageHeader const *src)
+{
+    if (!src) return Image_CT_None;
+    if (TinyImageFormat_IsFloat(src->format)) {
+        if ((flags & Image_CPF_AllowDXBC6and7) == 0) return Image_CT_None;
+    } else if (!TinyImageFormat_IsNormalised(src->format)) {
+        return Image_CT_None;
+    }
+    bool has_alpha = false;
+    switch (TinyImageFormat_ChannelCount(src->format)) {
+    case 1:
+        if (flags & Image_CPF_AllowDXBC1to5) return Image_CT_DXBC4;
+        break;
+    case 2:
+        if (flags & Image_CPF_AllowDXBC1to5) return Image_CT_DXBC5;
+        break;
+    case 3: break;
+    case 4: has_alpha = true; break;
+    }
+    if (flags & Image_CPF_AllowDXBC6and7) return Image_CT_DXBC7;
+    if (flags & Image_CPF_AllowASTC) return Image_CT_ASTC;
+    if (has_alpha) {
+        if (flags & Image_CPF_AllowDXBC1to5) return Image_CT_DXBC3;
+        if (flags & Image_CPF_AllowETC) return Image_CT_None;
+    } else {
+        if (flags & Image_CPF_AllowDXBC1to5) return Image_CT_DXBC1;
+        if (flags & Image_CPF_AllowETC) return Image_CT_None;
+    }
+    return Image_CT_None;
+}
+
+// ---- block level: one-block GPU launches (prefer gic_hip_encode_blocks_f32 for batches)
+
+static bool encode_one_block(gic_format fmt, const float *in, size_t nfloats, const gic_options &o, void *out,
+                             size_t out_bytes)
+{
+    DeviceScratch &s = t_scratch;
+    bool ok = s.reserve(nfloats * sizeof(float), out_bytes) &&
+              hipMemcpyAsync(s.src, in, nfloats * sizeof(float), hipMemcpyHostToDevice, s.stream) == hipSuccess &&
+              gic_hip_encode_blocks_f32(fmt, (const float *)s.src, 1, &o, (uint8_t *)s.dst, nullptr, s.stream) ==
+                  GIC_OK &&
+              hipMemcpyAsync(out, s.dst, out_bytes, hipMemcpyDeviceToHost, s.stream) == hipSuccess &&
+              hipStreamSynchronize(s.stream) == hipSuccess;
+    if (!ok) {
+        fprintf(stderr, "gfx_imagecompress_amd: block encode failed on the GPU\n");
+        memset(out, 0, out_bytes);
+    }
+    return ok;
+}
+
+extern "C" void Image_CompressAMDBC1Block(float const input[64], bool adaptive, bool b3d, uint8_t steps,
+                                          float alphaThreshold, void *out)
+{
+    gic_options o;
+    gic_default_options(&o);
+    o.adaptive_weights = adaptive;
+    o.b3d_refinement = b3d;
+    o.refinement_steps = steps;
+    o.bc1_alpha_threshold = alphaThreshold;
+    encode_one_block(GIC_FMT_BC1, input, 64, o, out, 8);
+}
+
+extern "C" void Image_CompressAMDAlphaSingleModeBlock(float const input[16], void *out)
+{
+    gic_options o;
+    gic_default_options(&o);
+    encode_one_block(GIC_FMT_BC4, input, 16, o, out, 8);
+}
+
+extern "C" void Image_CompressAMDMultiModeLDRBlock(float const input[64], uint8_t modeMask, bool srcHasAlpha,
+                                                   float quality, bool colourRestrict, bool alphaRestrict,
+                                                   float performance, void *out)
+{
+    (void)srcHasAlpha;   // unused by the reference encoder as well
+    gic_options o;
+    gic_default_options(&o);
+    o.bc7_mode_mask = modeMask;
+    o.bc7_quality = quality;
+    o.bc7_performance = performance;
+    o.colour_restrict = colourRestrict;
+    o.alpha_restrict = alphaRestrict;
+    encode_one_block(GIC_FMT_BC7, input, 64, o, out, 16);
+}
+
+// BC2/BC3 component blocks and the bc7enc16 block: not in this release.
+extern "C" void Image_CompressAMDRGBSingleModeBlock(float const *, bool, bool, uint8_t, void *out)
+{
+    fprintf(stderr, "gfx_imagecompress_amd: Image_CompressAMDRGBSingleModeBlock is not implemented\n");
+    memset(out, 0, 8);
+}
+extern "C" void Image_CompressAMDExplictAlphaSingleModeBlock(float const *, void *out)
+{
+    fprintf(stderr, "gfx_imagecompress_amd: Image_CompressAMDExplictAlphaSingleModeBlock is not implemented\n");
+    memset(out, 0, 8);
+}
+extern "C" void Image_CompressRichGel999BC7enc16(uint32_t const *, bool, bool, void *out)
+{
+    fprintf(stderr, "gfx_imagecompress_amd: Image_CompressRichGel999BC7enc16 is not implemented\n");
+    memset(out, 0, 16);
+}

@@ -1,0 +1,877 @@
+// gic_bcx.hip -- BC1 and BC4/BC5 block search for gfx950 (MI355X).
+//
+// Algorithm: the AMD Compressonator DXT search used by the reference
+// (src/amd_bcx_body.cpp, src/amd_bcx_helpers.cpp): PCA axis, 8x8 endpoint
+// ramp search on the projected axis with axis re-fitting, 565 grid snap,
+// per-channel 3x3 refinement, weighted clustering; BC4 is the 1-D window
+// search + hill climb of CompBlock1.  Results are bit-exact with the
+// reference: every float expression keeps the reference's types and
+// association order and the file is compiled with -ffp-contract=off.
+//
+// Mapping: one lane per 4x4 block (the work per block is a serial chain of
+// small data-dependent loops); 256-lane workgroups; the grid covers every
+// block of the launch.  Source texels are read as 16-byte rows so a wave's
+// 64 adjacent blocks issue fully coalesced 1 KiB row loads; each lane writes
+// one 8-byte (BC1/BC4) or 16-byte (BC5) block, coalesced across the wave.
+// The early-out of RampSrchW / RmpSrch1 is replaced by full evaluation: the
+// per-colour error terms are non-negative, so the partial sums are monotone
+// and "first strictly smaller" selection is unchanged.
+
+#include "gic_common.h"
+
+namespace gic {
+namespace bcx {
+
+enum { CH_B = 0, CH_G = 1, CH_R = 2, CH_A = 3 };
+
+__device__ __forceinline__ int chan_bits(int ch) { return ch == CH_G ? 6 : 5; }
+
+// MkRmpOnGrid, amd_bcx_body.cpp:122-151
+__device__ void snap_grid(float out[3][2], const float in[3][2])
+{
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        const float f1 = (float)(1 << chan_bits(ch));
+        const float f0 = (float)(1 << (8 - chan_bits(ch)));
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            float v = floorf(in[ch][e]);
+            if (v <= 0.f) {
+                v = 0.f;
+            } else {
+                v += floorf(128.f / f1) - floorf(v / f1);
+                v = minr(v, 255.f);
+            }
+            out[ch][e] = floorf(v / f0) * f0;
+        }
+    }
+}
+
+// MkWkRmpPts, amd_bcx_body.cpp:157-181
+__device__ __forceinline__ bool expand_grid(float out[3][2], const float in[3][2])
+{
+    bool flat = true;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) flat &= (in[ch][0] == in[ch][1]);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        const float f = (float)(1 << chan_bits(ch));
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            float v = in[ch][e] + floorf(in[ch][e] / f);
+            v = maxr(v, 0.f);
+            out[ch][e] = minr(v, 255.f);
+        }
+    }
+    return flat;
+}
+
+// BldClrRmp, amd_bcx_body.cpp:188-197 (n is 3 or 4)
+template <int N>
+__device__ __forceinline__ void chan_ramp(float r[4], const float ends[2])
+{
+    const float rnd = (N == 4) ? 1.f : 0.f;
+    r[0] = ends[0];
+    r[N - 1] = ends[1];
+    if (N & 1) r[N] = 1000000.f;
+#pragma unroll
+    for (int e = 1; e < N - 1; ++e)
+        r[e] = floorf((r[0] * (float)(N - 1 - e) + r[N - 1] * (float)e + rnd) / (float)(N - 1));
+}
+
+struct Colours {
+    float c[16][3];   // unique colours, B,G,R, x255
+    float rpt[16];    // repeat counts
+    int n;
+};
+
+// ClstrErr (weighted), amd_bcx_body.cpp:214-255
+template <int N>
+__device__ float ramp_fit_error(const Colours &u, const float r[3][4], bool flat)
+{
+    const float w0 = 0.3086f, w1 = 0.6094f, w2 = 0.0820f;
+    float err = 0.f;
+    const int nr = flat ? 1 : N;
+    for (int i = 0; i < u.n; ++i) {
+        float best = 99999999999.f;
+        for (int k = 0; k < nr; ++k) {
+            float d = (u.c[i][CH_R] - r[CH_R][k]) * (u.c[i][CH_R] - r[CH_R][k]) * w0 +
+                      (u.c[i][CH_G] - r[CH_G][k]) * (u.c[i][CH_G] - r[CH_G][k]) * w1 +
+                      (u.c[i][CH_B] - r[CH_B][k]) * (u.c[i][CH_B] - r[CH_B][k]) * w2;
+            if (d < best) best = d;
+        }
+        err += best * u.rpt[i];
+    }
+    return err;
+}
+
+// Refine, amd_bcx_body.cpp:582-806 (R, then G, then B 3x3 jitter of both
+// endpoints on the 565 grid; RefinementSteps = `steps`)
+template <int N>
+__device__ void refine_channels(float cur[3][2], const Colours &u, int steps)
+{
+    const float wr = 0.3086f, wg = 0.6094f, wb = 0.0820f;
+    float base[3][2], wk[3][2], r[3][4];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        base[ch][0] = cur[ch][0];
+        base[ch][1] = cur[ch][1];
+    }
+    bool flat = expand_grid(wk, cur);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) chan_ramp<N>(r[ch], wk[ch]);
+    float best = ramp_fit_error<N>(u, r, flat);
+    if (best == 0.f || !steps) return;
+    const int lo = -(int)minr((float)steps, 8.f), hi = (int)minr((float)steps, 8.f);
+    float side[4][16];
+#pragma unroll
+    for (int pass = 0; pass < 3; ++pass) {
+        const int ch = pass == 0 ? CH_R : pass == 1 ? CH_G : CH_B;
+        if (pass > 0) {
+            flat = expand_grid(wk, cur);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) chan_ramp<N>(r[c], wk[c]);
+        }
+        for (int i = 0; i < u.n; ++i)
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                if (ch == CH_R) {
+                    float dg = r[CH_G][k] - u.c[i][CH_G], db = r[CH_B][k] - u.c[i][CH_B];
+                    side[k][i] = dg * dg * wg + db * db * wb;
+                } else if (ch == CH_G) {
+                    float dr = r[CH_R][k] - u.c[i][CH_R], db = r[CH_B][k] - u.c[i][CH_B];
+                    side[k][i] = dr * dr * wr + db * db * wb;
+                } else {
+                    float dr = r[CH_R][k] - u.c[i][CH_R], dg = r[CH_G][k] - u.c[i][CH_G];
+                    side[k][i] = dr * dr * wr + dg * dg * wg;
+                }
+            }
+        const float grid = (float)(1 << (8 - chan_bits(ch)));
+        const float wc = (ch == CH_R) ? wr : (ch == CH_G) ? wg : wb;
+        float b0 = base[ch][0], b1 = base[ch][1];
+        for (int a = lo; a <= hi; ++a)
+            for (int b = lo; b <= hi; ++b) {
+                cur[ch][0] = minr(maxr(base[ch][0] + (float)a * grid, 0.f), 255.f);
+                cur[ch][1] = minr(maxr(base[ch][1] + (float)b * grid, 0.f), 255.f);
+                flat = expand_grid(wk, cur);
+                chan_ramp<N>(r[ch], wk[ch]);
+                float mse = 0.f;
+                const int nr = flat ? 1 : N;
+                for (int i = 0; i < u.n; ++i) {
+                    float m = 10000000.f;
+                    for (int k = 0; k < nr; ++k) {
+                        float d = r[ch][k] - u.c[i][ch];
+                        float e = side[k][i] + d * d * wc;
+                        m = minr(m, e);
+                    }
+                    mse += m * u.rpt[i];
+                }
+                if (mse < best) {
+                    b0 = cur[ch][0];
+                    b1 = cur[ch][1];
+                    best = mse;
+                }
+            }
+        cur[ch][0] = b0;
+        cur[ch][1] = b1;
+    }
+}
+
+// RampSrchW evaluated in full, amd_bcx_body.cpp:398-435
+template <int N>
+__device__ __forceinline__ float proj_ramp_error(const float *prj, const float *perr, const float *prem, float lo,
+                                                 float hi, int n)
+{
+    float error = 0;
+    const float step = (hi - lo) / (float)(N - 1);
+    const float step_h = step * (float)0.5;
+    const float rstep = (float)1.0f / step;
+    for (int i = 0; i < n; ++i) {
+        float v, del;
+        if ((del = prj[i] - lo) <= 0)
+            v = lo;
+        else if (prj[i] - hi >= 0)
+            v = hi;
+        else
+            v = floorf((del + step_h) * rstep) * step + lo;
+        float d = prj[i] - v;
+        d *= d;
+        error += prem[i] * d + perr[i];
+    }
+    return error;
+}
+
+// FindAxis, amd_bcx_body.cpp:442-570
+__device__ void principal_axis(float sh[16][3], float dir[3], float centre[3], bool &small, const float blk[16][3],
+                               const float *rpt, int n)
+{
+    float crr[3] = {0, 0, 0}, var[3] = {0, 0, 0};
+    dir[0] = dir[1] = dir[2] = 0.f;
+    centre[0] = centre[1] = centre[2] = 0.f;
+    float npts = 0.f;
+    for (int i = 0; i < n; ++i) {
+        centre[0] += blk[i][0] * rpt[i];
+        centre[1] += blk[i][1] * rpt[i];
+        centre[2] += blk[i][2] * rpt[i];
+        npts += rpt[i];
+    }
+    centre[0] /= npts;
+    centre[1] /= npts;
+    centre[2] /= npts;
+    for (int i = 0; i < n; ++i) {
+        sh[i][0] = blk[i][0] - centre[0];
+        sh[i][1] = blk[i][1] - centre[1];
+        sh[i][2] = blk[i][2] - centre[2];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            var[j] += sh[i][j] * sh[i][j] * rpt[i];
+            crr[j] += sh[i][j] * sh[i][(j + 1) % 3] * rpt[i];
+        }
+    }
+    int i0 = 0, k = 0;
+    float mx = 0.f;
+    const float eps = npts * (2.f / 255.f) * (2.f / 255.f);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        if (var[j] >= eps)
+            k++;
+        else
+            var[j] = 0.f;
+        if (mx < var[j]) {
+            mx = var[j];
+            i0 = j;
+        }
+    }
+    const float eps2 = npts * 3.f * (2.f / 255.f) * (2.f / 255.f);
+    small = (var[0] < eps2) && (var[1] < eps2) && (var[2] < eps2);
+    if (small) return;
+    if (k == 1) {
+        dir[i0] = 1.f;
+    } else if (k == 2) {
+        const int i1 = (var[(i0 + 1) % 3] > 0.f) ? (i0 + 1) % 3 : (i0 + 2) % 3;
+        const float cr = (i1 == (i0 + 1) % 3) ? crr[i0] : crr[(i0 + 2) % 3];
+        dir[i1] = cr / var[i0];
+        dir[i0] = 1.f;
+    } else {
+        float best_det = 100000.f;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const float det = var[j] * var[(j + 1) % 3] - crr[j] * crr[j];
+            if (best_det < det) {
+                best_det = det;
+                i0 = j;
+            }
+        }
+        const float a = var[(i0 + 1) % 3], b = -crr[i0], c = var[i0];
+        const float u0 = crr[(i0 + 2) % 3], u1 = crr[(i0 + 1) % 3];
+        float s0 = a * u0 + b * u1;
+        float s1 = b * u0 + c * u1;
+        s0 /= best_det;
+        s1 /= best_det;
+        dir[i0] = 1.f;
+        dir[(i0 + 1) % 3] = 1.f;
+        dir[(i0 + 2) % 3] = s0 + s1;
+    }
+    float len = dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2];
+    len = sqrtf(len);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) dir[j] = (len > 0.f) ? dir[j] / len : 0.f;
+}
+
+// CompressRGBBlockX, amd_bcx_body.cpp:937-1203
+template <int N>
+__device__ void fit_endpoints(float result[3][2], const Colours &u, int steps)
+{
+    float rc[3][2];
+    bool done = false;
+    if (u.n <= 2) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            rc[j][0] = u.c[0][j];
+            rc[j][1] = u.c[u.n - 1][j];
+        }
+        done = true;
+    }
+    float sh[16][3], mid[3], dir[3];
+    if (!done) {
+        float blk[16][3];
+        for (int i = 0; i < u.n; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) blk[i][j] = u.c[i][j] / 255.f;
+        bool small = true;
+        principal_axis(sh, dir, mid, small, blk, u.rpt, u.n);
+        if (small) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                rc[j][0] = u.c[0][j];
+                rc[j][1] = u.c[u.n - 1][j];
+            }
+            done = true;
+        }
+    }
+    if (!done) {
+        float err_g = 10000000.f;
+        float dir_g[3] = {0, 0, 0}, pos_g[2] = {0, 0};
+        float prj0[16], prj[16], perr[16], prem[16];
+        for (;;) {
+            float bnd0 = 1000.f, bnd1 = -1000.f;
+            for (int i = 0; i < u.n; ++i) {
+                prj0[i] = prj[i] = sh[i][0] * dir[0] + sh[i][1] * dir[1] + sh[i][2] * dir[2];
+                perr[i] = (sh[i][0] - dir[0] * prj[i]) * (sh[i][0] - dir[0] * prj[i]) +
+                          (sh[i][1] - dir[1] * prj[i]) * (sh[i][1] - dir[1] * prj[i]) +
+                          (sh[i][2] - dir[2] * prj[i]) * (sh[i][2] - dir[2] * prj[i]);
+                bnd0 = minr(bnd0, prj[i]);
+                bnd1 = maxr(bnd1, prj[i]);
+            }
+            const float scl0 = bnd0 - (bnd1 - bnd0) * 0.125f;
+            const float scl1 = bnd1 + (bnd1 - bnd0) * 0.125f;
+            const float scl2 = (scl1 - scl0) * (scl1 - scl0);
+            const float over = 1.f / (scl1 - scl0);
+            for (int i = 0; i < u.n; ++i) {
+                prj[i] = (prj[i] - scl0) * over;
+                prem[i] = u.rpt[i] * scl2;
+            }
+            bnd0 = (bnd0 - scl0) * over;
+            bnd1 = (bnd1 - scl0) * over;
+            const float stp = 0.025f;
+            const float ls = (bnd0 - 2.f * stp > 0.f) ? bnd0 - 2.f * stp : 0.f;
+            const float he = (bnd1 + 2.f * stp < 1.f) ? bnd1 + 2.f * stp : 1.f;
+            // 8x8 endpoint candidates, endpoints advanced by repeated adds
+            // exactly as the reference loop does (:1095-1097)
+            float err = 128000.f, pos0 = 0.f, pos1 = 0.f;
+            float lp = ls;
+            for (int l = 0; l < 8; ++l, lp += stp) {
+                float hp = he;
+                for (int h = 0; h < 8; ++h, hp -= stp) {
+                    const float e = proj_ramp_error<N>(prj, perr, prem, lp, hp, u.n);
+                    if (e < err) {
+                        err = e;
+                        pos0 = lp;
+                        pos1 = hp;
+                    }
+                }
+            }
+            pos0 = pos0 * (scl1 - scl0) + scl0;
+            pos1 = pos1 * (scl1 - scl0) + scl0;
+            if (!((double)err + 0.001 < (double)err_g)) break;
+            err_g = err;
+            dir_g[0] = dir[0];
+            dir_g[1] = dir[1];
+            dir_g[2] = dir[2];
+            pos_g[0] = pos0;
+            pos_g[1] = pos1;
+            const float step = (pos1 - pos0) / (float)(N - 1);
+            const float step_h = step * (float)0.5;
+            const float rstep = (float)1.0f / step;
+            const float over_n = 1.f / (float)(N - 1);
+            const float avg = (float)(N - 1) / 2.f;
+            float crs[3] = {0, 0, 0}, len = 0.f;
+            for (int i = 0; i < u.n; ++i) {
+                float ri, del;
+                if ((del = prj0[i] - pos0) <= 0)
+                    ri = 0.f;
+                else if (prj0[i] - pos1 >= 0)
+                    ri = (float)(N - 1);
+                else
+                    ri = floorf((del + step_h) * rstep);
+                ri = (ri - avg) * over_n;
+                const float pm = ri * u.rpt[i];
+                len += ri * pm;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) crs[j] += sh[i][j] * pm;
+            }
+            dir[0] = dir[1] = dir[2] = 0.f;
+            if (len > 0.f) {
+                dir[0] = crs[0] / len;
+                dir[1] = crs[1] / len;
+                dir[2] = crs[2] / len;
+                float l2 = dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2];
+                l2 = sqrtf(l2);
+                dir[0] /= l2;
+                dir[1] /= l2;
+                dir[2] /= l2;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) rc[j][k] = (pos_g[k] * dir_g[j] + mid[j]) * 255.f;
+    }
+    snap_grid(result, rc);
+    refine_channels<N>(result, u, steps);
+}
+
+// Unique colours of the texels kept by the alpha test, sorted by the R,G,B
+// bit patterns (QSortFloatCmp, amd_bcx_body.cpp:103-117) with repeat counts
+// (:1242-1262).  Works by ranking instead of moving records.
+__device__ void unique_colours(Colours &u, const float in[64], bool use_alpha, float thr01, int &kept)
+{
+    uint32_t key[16][3];
+    bool live[16];
+    kept = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        live[i] = !use_alpha || (in[i * 4 + 3] >= thr01);
+        key[i][0] = __float_as_uint(in[i * 4 + 2]);   // B
+        key[i][1] = __float_as_uint(in[i * 4 + 1]);   // G
+        key[i][2] = __float_as_uint(in[i * 4 + 0]);   // R
+        kept += live[i] ? 1 : 0;
+    }
+    // a live texel leads its colour group if no earlier live texel has the same key
+    int rank[16], cnt[16];
+    bool lead[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        int less = 0, same_before = 0, same = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (!live[j]) continue;
+            const bool eq = key[j][0] == key[i][0] && key[j][1] == key[i][1] && key[j][2] == key[i][2];
+            const bool lt = key[j][2] < key[i][2] ||
+                            (key[j][2] == key[i][2] &&
+                             (key[j][1] < key[i][1] || (key[j][1] == key[i][1] && key[j][0] < key[i][0])));
+            same += eq ? 1 : 0;
+            same_before += (eq && j < i) ? 1 : 0;
+            less += lt ? 1 : 0;
+        }
+        lead[i] = live[i] && same_before == 0;
+        cnt[i] = same;
+        rank[i] = less;   // number of live texels with a smaller key
+    }
+    // unique index of a leader = number of leaders with a smaller key
+    u.n = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (!lead[i]) continue;
+        int ui = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) ui += (lead[j] && (rank[j] < rank[i])) ? 1 : 0;
+        u.c[ui][0] = (float)((double)in[i * 4 + 2] * 255.0);
+        u.c[ui][1] = (float)((double)in[i * 4 + 1] * 255.0);
+        u.c[ui][2] = (float)((double)in[i * 4 + 0] * 255.0);
+        u.rpt[ui] = (float)cnt[i];
+        u.n++;
+    }
+}
+
+// Clstr -> ClstrBas -> ClstrIntnl, amd_bcx_body.cpp:258-378
+template <int N>
+__device__ uint32_t final_indices(const float in[64], const uint8_t ep[3][2], bool use_alpha, float thr01, float &err)
+{
+    const float w0 = 0.3086f, w1 = 0.6094f, w2 = 0.0820f;
+    const unsigned c0 = ((unsigned)(ep[CH_R][0] & 0xf8) << 8) | ((unsigned)(ep[CH_G][0] & 0xfc) << 3) |
+                        ((unsigned)(ep[CH_B][0] & 0xf8) >> 3);
+    const unsigned c1 = ((unsigned)(ep[CH_R][1] & 0xf8) << 8) | ((unsigned)(ep[CH_G][1] & 0xfc) << 3) |
+                        ((unsigned)(ep[CH_B][1] & 0xf8) >> 3);
+    const bool swap = (!(N & 1) && c0 <= c1) || ((N & 1) && c0 > c1);
+    float ends[3][2], wk[3][2], r[3][4];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        ends[ch][0] = (float)ep[ch][swap ? 1 : 0];
+        ends[ch][1] = (float)ep[ch][swap ? 0 : 1];
+    }
+    const bool flat = expand_grid(wk, ends);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) chan_ramp<N>(r[ch], wk[ch]);
+    const float thr = thr01 * 255.f;
+    const int nr = flat ? 1 : N;
+    uint32_t bits = 0;
+    err = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const float R = in[i * 4 + 0] * 255.0f, G = in[i * 4 + 1] * 255.0f, B = in[i * 4 + 2] * 255.0f;
+        const float A = in[i * 4 + 3] * 255.0f;
+        uint32_t idx;
+        if (use_alpha && !(A >= thr)) {
+            idx = N;
+        } else {
+            float best = 99999999999.f;
+            int bi = 0;
+            for (int k = 0; k < nr; ++k) {
+                const float d = (R - r[CH_R][k]) * (R - r[CH_R][k]) * w0 + (G - r[CH_G][k]) * (G - r[CH_G][k]) * w1 +
+                                (B - r[CH_B][k]) * (B - r[CH_B][k]) * w2;
+                if (d < best) {
+                    best = d;
+                    bi = k;
+                }
+            }
+            err += best;
+            if (bi == N - 1)
+                bi = 1;
+            else if (bi)
+                bi++;
+            idx = (uint32_t)bi;
+        }
+        bits |= (idx & 3u) << (2 * i);
+    }
+    return bits;
+}
+
+// CompRGBABlock, amd_bcx_body.cpp:1209-1297.  Returns the float error (FLT_MAX
+// for a 4-colour ramp over transparent texels).
+template <int N>
+__device__ float comp_rgba(const float in[64], int steps, bool use_alpha, float thr01, uint8_t ep[3][2],
+                           uint32_t &ibits, const Colours &u, int kept)
+{
+    if (!kept) {
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            ep[ch][0] = 0;
+            ep[ch][1] = 0xff;
+        }
+        ibits = 0xffffffffu;
+        return 0.f;
+    }
+    if (kept != 16 && use_alpha && !(N & 1)) return 3.402823466e+38f;
+    float res[3][2];
+    fit_endpoints<N>(res, u, steps);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        ep[ch][0] = (uint8_t)res[ch][0];
+        ep[ch][1] = (uint8_t)res[ch][1];
+    }
+    float err;
+    ibits = final_indices<N>(in, ep, use_alpha, thr01, err);
+    return err;
+}
+
+// Image_CompressAMDBC1Block, amd_bcx_helpers.cpp:51-105
+__device__ uint2 encode_bc1(const float in[64], int steps, float thr01)
+{
+    const bool use_alpha = thr01 > 0.0f;
+    Colours u;
+    int kept;
+    unique_colours(u, in, use_alpha, thr01, kept);
+    uint8_t ep3[3][2], ep4[3][2];
+    uint32_t i3 = 0, i4 = 0;
+    const double e3 = comp_rgba<3>(in, steps, use_alpha, thr01, ep3, i3, u, kept);
+    double e4 = 3.402823466e+38;
+    if (!(e3 == 0.0)) e4 = comp_rgba<4>(in, steps, use_alpha, thr01, ep4, i4, u, kept);
+    const bool m4 = !(e3 <= e4);
+    const uint8_t(*ep)[2] = m4 ? ep4 : ep3;
+    const unsigned c0 = ((unsigned)(ep[CH_R][0] >> 3) << 11) | ((unsigned)(ep[CH_G][0] >> 2) << 5) |
+                        (unsigned)(ep[CH_B][0] >> 3);
+    const unsigned c1 = ((unsigned)(ep[CH_R][1] >> 3) << 11) | ((unsigned)(ep[CH_G][1] >> 2) << 5) |
+                        (unsigned)(ep[CH_B][1] >> 3);
+    uint2 out;
+    if ((m4 && c0 <= c1) || (!m4 && c0 > c1))
+        out.x = c1 | (c0 << 16);
+    else
+        out.x = c0 | (c1 << 16);
+    out.y = m4 ? i4 : i3;
+    return out;
+}
+
+// ------------------------------------------------------------- BC4 ---
+
+// RmpSrch1 evaluated in full, amd_bcx_body.cpp:1510-1548
+template <int N>
+__device__ __forceinline__ float scalar_ramp_error(const float *v, const float *rpt, float lo, float hi, int nv)
+{
+    float error = 0;
+    const float step = (hi - lo) / (float)(N - 1);
+    const float step_h = step * 0.5f;
+    const float rstep = 1.0f / step;
+    for (int i = 0; i < nv; ++i) {
+        float q, del;
+        if ((del = v[i] - lo) <= 0)
+            q = lo;
+        else if (v[i] - hi >= 0)
+            q = hi;
+        else
+            q = (floorf((del + step_h) * rstep) * step) + lo;
+        const float d = v[i] - q;
+        error += d * d * rpt[i];
+    }
+    return error;
+}
+
+// CompBlock1 (8-bit integer grid), amd_bcx_body.cpp:1633-1832
+template <int N, bool FIXED>
+__device__ void scalar_endpoints(float ramp[2], const float vals_sorted[16])
+{
+    float uv[16], ur[16];
+    int nu = 0;
+    bool need = true;
+    float prev = -2.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const float x = vals_sorted[i];
+        if (FIXED) {
+            if (prev != x) {
+                prev = x;
+                if (!((double)prev <= 1.5 / 255.) && !((double)prev >= 253.5 / 255.)) {
+                    uv[nu] = x;
+                    ur[nu] = 1.f;
+                    nu++;
+                }
+            } else if (nu > 0 && uv[nu - 1] == prev) {
+                ur[nu - 1] += 1.f;
+            }
+        } else {
+            if (prev != x) {
+                uv[nu] = prev = x;
+                ur[nu] = 1.f;
+                nu++;
+            } else {
+                ur[nu - 1] += 1.f;
+            }
+        }
+    }
+    if (nu <= 2) {
+        if (FIXED && nu == 0) {
+            ramp[0] = 128.f;
+            ramp[1] = ramp[0] + 1.f;
+        } else {
+            ramp[0] = floorf(uv[0] * 255.f + 0.5f);
+            ramp[1] = (nu == 1) ? ramp[0] + 1.f : floorf(uv[1] * 255.f + 0.5f);
+        }
+        need = false;
+    }
+    if (need) {
+        float lo = uv[0], hi = uv[nu - 1];
+        float lr = lo, hr = hi, gl = 0, gr = 0;
+        const float cntr = (lr + hr) / 2;
+        float gerr = 128000.f;
+        if (!(hi - lo <= 48.f / 256.f)) {
+            const float llb = (0.f > lr - 0.1f) ? 0.f : lr - 0.1f;
+            const float rrb = (1.f < hr + 0.1f) ? 1.f : hr + 0.1f;
+            const float lrb = (cntr < lr + 0.1f) ? cntr : lr + 0.1f;
+            const float rlb = (cntr > hr - 0.1f) ? cntr : hr - 0.1f;
+            for (float sl = llb; sl < lrb; sl += 0.018f)
+                for (float sr = rrb; rlb <= sr; sr -= 0.018f) {
+                    const float e = scalar_ramp_error<N>(uv, ur, sl, sr, nu);
+                    if (e < gerr) {
+                        gerr = e;
+                        gl = sl;
+                        gr = sr;
+                    }
+                }
+            lr = gl;
+            hr = gr;
+        }
+        // Refine1 hill climb, amd_bcx_body.cpp:1555-1607
+        const float mstep = 0.6f / 256.f;
+        const float mv[3] = {0.f, -1.f, 1.f};
+        int bm;
+        do {
+            float ca0 = lr, cb0 = hr;
+            bm = -1;
+#pragma unroll
+            for (int m = 0; m < 9; ++m) {
+                float ca = lr + mstep * mv[m / 3];
+                float cb = hr + mstep * mv[m % 3];
+                ca = maxr(ca, 0.f);
+                cb = minr(cb, 1.f);
+                const float e = scalar_ramp_error<N>(uv, ur, ca, cb, nu);
+                if (e < gerr) {
+                    gerr = e;
+                    bm = m;
+                    ca0 = ca;
+                    cb0 = cb;
+                }
+            }
+            if (bm != -1) {
+                lr = ca0;
+                hr = cb0;
+            }
+        } while (bm != -1);
+        lo = lr * 255.f;
+        hi = hr * 255.f;
+        ramp[1] = floorf(hi + 0.5f);
+        ramp[0] = floorf(lo + 0.5f);
+    }
+    if (ramp[0] == ramp[1]) {
+        if (ramp[1] < 255.f)
+            ramp[1]++;
+        else
+            ramp[1]--;
+    }
+}
+
+// GetRmp1 + BldRmp1 + Clstr1, amd_bcx_body.cpp:1395-1505 (endpoint swap kept)
+template <int N, bool FIXED>
+__device__ float scalar_cluster(const float v[16], float ramp[2], uint64_t &ibits)
+{
+    ibits = 0;
+    float err = 0.f;
+    if (ramp[0] == ramp[1]) return err;
+    if ((!FIXED && ramp[0] <= ramp[1]) || (FIXED && ramp[0] > ramp[1])) {
+        const float t = ramp[0];
+        ramp[0] = ramp[1];
+        ramp[1] = t;
+    }
+    constexpr int NP = FIXED ? N + 2 : N;
+    float pts[NP];
+    pts[0] = ramp[0];
+    pts[1] = ramp[1];
+#pragma unroll
+    for (int e = 1; e < N - 1; ++e)
+        pts[e + 1] = (pts[0] * (float)(N - 1 - e) + pts[1] * (float)e) / (float)(N - 1);
+    if (FIXED) {
+        pts[N] = 0.f;
+        pts[N + 1] = 255.f;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) pts[i] = floorf(pts[i] + 0.5f) / 1.f;
+    const float over = 1.f / ((float)(1 << 8) - 1.f);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) pts[i] *= over;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        float best = 10000000.f;
+        int bi = 0;
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            float d = v[i] - pts[j];
+            d *= d;
+            if (d < best) {
+                best = d;
+                bi = j;
+            }
+        }
+        err += best;
+        ibits |= (uint64_t)bi << (3 * i);
+    }
+    return err;
+}
+
+template <int N, bool FIXED>
+__device__ float scalar_block(const float v[16], const float sorted[16], uint8_t ep[2], uint64_t &ibits)
+{
+    float ramp[2];
+    scalar_endpoints<N, FIXED>(ramp, sorted);
+    const float err = scalar_cluster<N, FIXED>(v, ramp, ibits);
+    ep[0] = (uint8_t)ramp[0];
+    ep[1] = (uint8_t)ramp[1];
+    return err;
+}
+
+// Image_CompressAMDAlphaSingleModeBlock + EncodeAlphaBlock,
+// amd_bcx_helpers.cpp:32-46, :125-140
+__device__ uint64_t encode_bc4(const float v[16])
+{
+    // ascending sort by rank (equal values are interchangeable)
+    float s[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        int r = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) r += (v[j] < v[i] || (v[j] == v[i] && j < i)) ? 1 : 0;
+        // scatter through a select chain keeps s[] in registers
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (r == k) s[k] = v[i];
+    }
+    uint8_t ep8[2], ep6[2];
+    uint64_t i8, i6 = 0;
+    const float e8 = scalar_block<8, false>(v, s, ep8, i8);
+    float e6 = 3.402823466e+38f;
+    if (!(e8 == 0.f)) e6 = scalar_block<6, true>(v, s, ep6, i6);
+    const bool use8 = e8 <= e6;
+    const uint8_t *ep = use8 ? ep8 : ep6;
+    return (uint64_t)ep[0] | ((uint64_t)ep[1] << 8) | ((use8 ? i8 : i6) << 16);
+}
+
+}  // namespace bcx
+
+// ------------------------------------------------------------- kernels ---
+
+struct Bc1Params {
+    float alpha_threshold;
+    int steps;
+    int force_alpha_one;
+};
+
+__global__ void __launch_bounds__(256) bc1_image_kernel(Geometry g, Bc1Params p, uint2 *__restrict__ dst)
+{
+    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= g.total) return;
+    uint32_t slice, by, bx;
+    block_coords(g, id, slice, by, bx);
+    float blk[64];
+    load_block(g, slice, by, bx, p.force_alpha_one != 0, blk);
+    dst[id] = bcx::encode_bc1(blk, p.steps, p.alpha_threshold);
+}
+
+__global__ void __launch_bounds__(256) bc45_image_kernel(Geometry g, int fmt, int channel,
+                                                         uint64_t *__restrict__ dst)
+{
+    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= g.total) return;
+    uint32_t slice, by, bx;
+    block_coords(g, id, slice, by, bx);
+    float blk[64], v[16];
+    load_block(g, slice, by, bx, false, blk);
+    if (fmt == 4) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = blk[i * 4 + channel];
+        dst[id] = bcx::encode_bc4(v);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = blk[i * 4 + 0];
+        const uint64_t r = bcx::encode_bc4(v);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = blk[i * 4 + 1];
+        const uint64_t gch = bcx::encode_bc4(v);
+        dst[2 * (size_t)id] = r;
+        dst[2 * (size_t)id + 1] = gch;
+    }
+}
+
+__global__ void __launch_bounds__(256) bc1_blocks_kernel(const float *__restrict__ blocks, uint32_t n, Bc1Params p,
+                                                         uint2 *__restrict__ dst)
+{
+    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= n) return;
+    float blk[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) blk[i] = blocks[(size_t)id * 64 + i];
+    dst[id] = bcx::encode_bc1(blk, p.steps, p.alpha_threshold);
+}
+
+__global__ void __launch_bounds__(256) bc4_blocks_kernel(const float *__restrict__ blocks, uint32_t n,
+                                                         uint64_t *__restrict__ dst)
+{
+    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= n) return;
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = blocks[(size_t)id * 16 + i];
+    dst[id] = bcx::encode_bc4(v);
+}
+
+// ------------------------------------------------------------ launchers ---
+
+hipError_t launch_bc1_image(const Geometry &g, float thr, int steps, int force_alpha_one, void *dst,
+                            hipStream_t s)
+{
+    const Bc1Params p{thr, steps, force_alpha_one};
+    const uint32_t wg = 256, grid = (g.total + wg - 1) / wg;
+    hipLaunchKernelGGL(bc1_image_kernel, dim3(grid), dim3(wg), 0, s, g, p, (uint2 *)dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_bc45_image(const Geometry &g, int fmt, int channel, void *dst, hipStream_t s)
+{
+    const uint32_t wg = 256, grid = (g.total + wg - 1) / wg;
+    hipLaunchKernelGGL(bc45_image_kernel, dim3(grid), dim3(wg), 0, s, g, fmt, channel, (uint64_t *)dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_bc1_blocks(const float *blocks, uint32_t n, float thr, int steps, void *dst, hipStream_t s)
+{
+    const Bc1Params p{thr, steps, 0};
+    const uint32_t wg = 256, grid = (n + wg - 1) / wg;
+    hipLaunchKernelGGL(bc1_blocks_kernel, dim3(grid), dim3(wg), 0, s, blocks, n, p, (uint2 *)dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_bc4_blocks(const float *blocks, uint32_t n, void *dst, hipStream_t s)
+{
+    const uint32_t wg = 256, grid = (n + wg - 1) / wg;
+    hipLaunchKernelGGL(bc4_blocks_kernel, dim3(grid), dim3(wg), 0, s, blocks, n, (uint64_t *)dst);
+    return hipGetLastError();
+}
+
+}  // namespace gic

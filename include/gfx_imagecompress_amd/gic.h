@@ -1,0 +1,97 @@
+/*
+ * gic.h -- batched device entry points of the MI355X BCn compressor.
+ *
+ * C ABI only: plain pointers, sizes and a stream handle (a hipStream_t passed
+ * as void*; NULL = the legacy default stream).  All pointers named d_* are
+ * device (HBM) pointers.  These are the "new batched device entry" of
+ * SURVEY.md section 8(b); the reference has no equivalent because its block
+ * loop runs on the host (src/amd_bc1_compressor.cpp:44-70 and siblings).
+ *
+ * Return value: 0 on success, a negative number on error:
+ *   GIC_EINVAL   bad argument (shape, pointer, option out of range)
+ *   GIC_EUNSUP   option outside the implemented default-quality path
+ *   GIC_EHIP     a HIP runtime call failed (see gic_last_hip_error())
+ */
+#ifndef GFX_IMAGECOMPRESS_AMD_GIC_H_
+#define GFX_IMAGECOMPRESS_AMD_GIC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GIC_OK 0
+#define GIC_EINVAL (-1)
+#define GIC_EUNSUP (-2)
+#define GIC_EHIP (-3)
+
+typedef enum gic_format {
+    GIC_FMT_BC1 = 1, /* Image_CompressAMDBC1Block semantics (amd_bcx_helpers.cpp:51) */
+    GIC_FMT_BC4 = 4, /* Image_CompressAMDAlphaSingleModeBlock on one channel (:125) */
+    GIC_FMT_BC5 = 5, /* two BC4 blocks, channel 0 then channel 1 (amd_bc5_compressor.cpp:35-41) */
+    GIC_FMT_BC7 = 7  /* BC7BlockEncoder::CompressBlock (amd_bc7_body.cpp:1289) */
+} gic_format;
+
+/* Options; gic_default_options() gives the reference defaults
+ * (Image_CompressDefaultAmdOptions, amd_bcx_helpers.cpp:23-31; BC1 options,
+ * amd_bc1_compressor.cpp:21-27; BC7 wrapper arguments, amd_bc7_compressor.cpp:58-65). */
+typedef struct gic_options {
+    uint32_t struct_size;        /* sizeof(gic_options) */
+    float bc1_alpha_threshold;   /* 0..1; <= 0 disables punch-through (default 128/255) */
+    uint8_t refinement_steps;    /* AMD RefinementSteps, 0..8 (default 1) */
+    uint8_t b3d_refinement;      /* must be 0 (Refine3D not implemented) */
+    uint8_t adaptive_weights;    /* must be 0 (reference path is UB: block_utils.cpp:201-203) */
+    uint8_t bc4_channel;         /* source channel for BC4 (reference reads 1: amd_bc4_compressor.cpp:34) */
+    uint8_t bc7_mode_mask;       /* default 0xFF (0 means 0xCF, amd_bc7_body.hpp:103-106) */
+    uint8_t colour_restrict;     /* default 1 */
+    uint8_t alpha_restrict;      /* default 1 */
+    uint8_t force_alpha_one;     /* 1: ignore source alpha (ReadNxNBlockF forceAlphaTo1) */
+    float bc7_quality;           /* must be 1.0 in this release */
+    float bc7_performance;       /* must be 1.0 in this release */
+} gic_options;
+
+void gic_default_options(gic_options *opt);
+
+/* Bytes per 4x4 block of a format (8 or 16). */
+uint32_t gic_block_bytes(gic_format fmt);
+
+/* Encode a slice stack of 8-bit images resident in HBM.
+ *   d_src: slices x height rows of row_pitch bytes, each texel `channels`
+ *          bytes (1..4, R[G[B[A]]]), slice pitch = row_pitch * height.
+ *   d_dst: blocks in row-major order per slice, slices stacked
+ *          (ceil(w/4) * ceil(h/4) * slices * gic_block_bytes).
+ *   d_block_err: optional (NULL) per-block error (BC7: the encoder's error).
+ * Partial edge blocks replicate the last row/column (block_utils.cpp:19-22).
+ * The launch is asynchronous on `stream`. */
+int gic_hip_encode(gic_format fmt, const uint8_t *d_src, uint32_t width, uint32_t height,
+                   uint32_t slices, uint32_t channels, size_t row_pitch, const gic_options *opt,
+                   uint8_t *d_dst, double *d_block_err, void *stream);
+
+/* Same, restricted to block rows [first_block_row, first_block_row+num_block_rows)
+ * of every slice; d_dst receives only those rows (contiguous per slice, slices
+ * stacked).  This is the per-rank shard of the multi-GPU path. */
+int gic_hip_encode_rows(gic_format fmt, const uint8_t *d_src, uint32_t width, uint32_t height,
+                        uint32_t slices, uint32_t channels, size_t row_pitch,
+                        uint32_t first_block_row, uint32_t num_block_rows, const gic_options *opt,
+                        uint8_t *d_dst, double *d_block_err, void *stream);
+
+/* Block-level batch: n blocks of 16 texels, float in [0,1].
+ *   BC1/BC7: d_blocks holds n x 64 floats (RGBA per texel, texel-major).
+ *   BC4:     d_blocks holds n x 16 floats.
+ * This is the batched form of the reference's block API
+ * (imagecompress.h:111-136). */
+int gic_hip_encode_blocks_f32(gic_format fmt, const float *d_blocks, uint32_t n, const gic_options *opt,
+                              uint8_t *d_dst, double *d_block_err, void *stream);
+
+/* Last HIP error code recorded by this thread (0 if none). */
+int gic_last_hip_error(void);
+
+/* Library version string. */
+const char *gic_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Regenerate the golden vectors in tests/golden/ from the CPU restatement.
+
+Inputs are re-created from gfx_imagecompress_amd.synth (deterministic), so only
+encoded outputs (and BC7 per-block encoder errors) are stored.  manifest.json
+records the FNV-1a-64 of every output and the recipe that produced it.
+Run from the repo root:  python tests/golden/make_golden.py
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+sys.path.insert(0, os.path.dirname(HERE))
+
+from gfx_imagecompress_amd import synth  # noqa: E402
+import oracle_lib  # noqa: E402
+
+
+def cases():
+    """name -> (fmt, image, kwargs).  Kept small (< 150 KB total)."""
+    yield "bc1_g0_256", 1, synth.g0(256, 256), {}
+    yield "bc1_g1_256", 1, synth.g1(256, 256), {}
+    yield "bc1_pattern_37", 1, synth.reference_pattern_rgb(37, 37), {}
+    yield "bc1_punch_64", 1, synth.reference_pattern_rgb(64, 64, punch_through=True), {}
+    yield "bc1_noise_alpha_32", 1, synth.noise_rgba(32, 32, seed=7, alpha=True), {}
+    yield "bc4_height_128_ch0", 4, synth.height_field(128, 128, seed=1), {"bc4_channel": 0}
+    yield "bc4_g1_64_ch1", 4, synth.g1(64, 64), {"bc4_channel": 1}
+    yield "bc5_g0_256", 5, synth.g0(256, 256), {}
+    yield "bc5_normal_128", 5, synth.normal_map(synth.height_field(128, 128, seed=1)), {}
+    yield "bc7_g0_256_rows0_2", 7, synth.g0(256, 256), {"first_row": 0, "num_rows": 2}
+    yield "bc7_g1_256_rows0_2", 7, synth.g1(256, 256), {"first_row": 0, "num_rows": 2}
+    yield "bc7_pattern_alpha_16", 7, synth.reference_pattern_rgb(16, 16, alpha_ramp=True), {}
+    yield "bc7_punch_16", 7, synth.reference_pattern_rgb(16, 16, punch_through=True)[4:, 4:], {}
+    yield "bc7_noise_alpha_16", 7, synth.noise_rgba(16, 16, seed=3, alpha=True), {}
+
+
+def main():
+    manifest = {}
+    for name, fmt, img, kw in cases():
+        want_err = fmt == 7
+        res = oracle_lib.encode_image(fmt, img, want_err=want_err, **kw)
+        out, err = (res if want_err else (res, None))
+        out.tofile(os.path.join(HERE, name + ".bin"))
+        entry = {"fmt": fmt, "shape": list(img.shape), "kwargs": kw, "blocks": int(out.shape[0]),
+                 "fnv1a64": "%016x" % oracle_lib.fnv1a64(out)}
+        if err is not None:
+            err.astype(np.float64).tofile(os.path.join(HERE, name + ".err.f64"))
+        manifest[name] = entry
+        print(name, entry["fnv1a64"], out.shape)
+    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

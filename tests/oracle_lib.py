@@ -1,0 +1,106 @@
+"""ctypes binding of the CPU restatement (oracle/liboracle_bcn.so).
+
+TEST INFRASTRUCTURE ONLY: tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg are the only users; the product never loads the oracle.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle_bcn.so")
+
+_lib = None
+
+
+def build() -> str:
+    if not os.path.exists(ORACLE_SO):
+        subprocess.run(["make", "-C", ORACLE_DIR, "-s"], check=True)
+    return ORACLE_SO
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        _lib = ctypes.CDLL(build())
+        vp = ctypes.c_void_p
+        _lib.orc_encode_image.argtypes = [ctypes.c_int, vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.c_uint32, ctypes.c_int, ctypes.c_int32, ctypes.c_int32,
+                                          ctypes.c_int, vp, vp]
+        _lib.orc_encode_image.restype = ctypes.c_int
+        _lib.orc_bc1_block.argtypes = [vp, ctypes.c_int, ctypes.c_float, vp]
+        _lib.orc_bc4_block.argtypes = [vp, vp]
+        _lib.orc_bc7_block.argtypes = [vp, ctypes.c_uint8, ctypes.c_int, ctypes.c_float, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_float, vp]
+        _lib.orc_bc7_block.restype = ctypes.c_double
+        _lib.orc_fnv1a64.argtypes = [vp, ctypes.c_size_t]
+        _lib.orc_fnv1a64.restype = ctypes.c_uint64
+        _lib.orc_bc7_shake_ramp.argtypes = [ctypes.c_int] * 5
+        _lib.orc_bc7_shake_ramp.restype = ctypes.c_int
+        _lib.orc_bc7_decode.argtypes = [vp, vp]
+    return _lib
+
+
+def block_bytes(fmt: int) -> int:
+    return 8 if fmt in (1, 4) else 16
+
+
+def encode_image(fmt: int, img: np.ndarray, bc4_channel: int = 1, first_row: int = -1, num_rows: int = -1,
+                 threads: int = 0, want_err: bool = False):
+    """img: (H,W,C) or (S,H,W,C) uint8.  Returns uint8 blocks (S*rows*bx, bytes) [, errors]."""
+    a = np.ascontiguousarray(img, dtype=np.uint8)
+    if a.ndim == 2:
+        a = a[:, :, None]
+    if a.ndim == 3:
+        a = a[None]
+    s, h, w, c = a.shape
+    bx, by = (w + 3) // 4, (h + 3) // 4
+    rows = by - max(first_row, 0) if num_rows < 0 else num_rows
+    out = np.zeros((s * rows * bx, block_bytes(fmt)), np.uint8)
+    err = np.zeros(s * rows * bx, np.float64) if want_err else None
+    threads = threads or min(os.cpu_count() or 1, 16)
+    rc = lib().orc_encode_image(fmt, a.ctypes.data, w, h, s, c, bc4_channel, first_row, num_rows, threads,
+                                out.ctypes.data, err.ctypes.data if want_err else None)
+    if rc != 0:
+        raise RuntimeError(f"oracle encode failed ({rc})")
+    return (out, err) if want_err else out
+
+
+def bc1_block(block: np.ndarray, steps: int = 1, threshold: float = 128 / 255.0) -> bytes:
+    b = np.ascontiguousarray(block, dtype=np.float32).reshape(64)
+    out = np.zeros(8, np.uint8)
+    lib().orc_bc1_block(b.ctypes.data, steps, threshold, out.ctypes.data)
+    return out.tobytes()
+
+
+def bc4_block(values: np.ndarray) -> bytes:
+    v = np.ascontiguousarray(values, dtype=np.float32).reshape(16)
+    out = np.zeros(8, np.uint8)
+    lib().orc_bc4_block(v.ctypes.data, out.ctypes.data)
+    return out.tobytes()
+
+
+def bc7_block(block: np.ndarray, mode_mask: int = 0xFF):
+    b = np.ascontiguousarray(block, dtype=np.float32).reshape(64)
+    out = np.zeros(16, np.uint8)
+    e = lib().orc_bc7_block(b.ctypes.data, mode_mask, 1, 1.0, 1, 1, 1.0, out.ctypes.data)
+    return out.tobytes(), e
+
+
+def bc7_decode(blocks: np.ndarray) -> np.ndarray:
+    """(n,16) uint8 -> (n,16,4) uint8 RGBA."""
+    b = np.ascontiguousarray(blocks, dtype=np.uint8).reshape(-1, 16)
+    out = np.zeros((b.shape[0], 16, 4), np.uint8)
+    for i in range(b.shape[0]):
+        lib().orc_bc7_decode(b[i].ctypes.data, out[i].ctypes.data)
+    return out
+
+
+def fnv1a64(data: np.ndarray) -> int:
+    a = np.ascontiguousarray(data).view(np.uint8)
+    return int(lib().orc_fnv1a64(a.ctypes.data, a.size))

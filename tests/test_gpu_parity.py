@@ -1,0 +1,209 @@
+"""GPU parity tests: the HIP kernels (through the C ABI) against the oracle.
+
+Bar: bit-exact for BC1/BC4/BC5.  Inputs are seeded; sizes
+where the oracle finishes in seconds are compared block-for-block, the 8K
+configurations likewise (the oracle runs multi-threaded).
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+import gfx_imagecompress_amd as gic
+import oracle_lib
+from gfx_imagecompress_amd import synth
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def gpu_encode(fmt, img, options=None, first_row=0, num_rows=None, err=False):
+    import torch
+    a = np.ascontiguousarray(img, dtype=np.uint8)
+    if a.ndim == 2:
+        a = a[:, :, None]
+    if a.ndim == 3:
+        a = a[None]
+    s, h, w, c = a.shape
+    bx, by = gic.blocks_shape(w, h)
+    rows = by - first_row if num_rows is None else num_rows
+    src = torch.from_numpy(a).cuda()
+    dst = torch.zeros(bx * rows * s * gic.block_bytes(fmt), dtype=torch.uint8, device="cuda")
+    e = torch.zeros(bx * rows * s, dtype=torch.float64, device="cuda") if err else None
+    opts = options or gic.Options()
+    if fmt in (gic.FMT_BC1, gic.FMT_BC7) and c < 4:
+        opts.force_alpha_one = True
+    gic.encode_device(fmt, src, w, h, s, c, dst, opts, first_block_row=first_row, num_block_rows=rows,
+                      block_err=e)
+    torch.cuda.synchronize()
+    out = dst.cpu().numpy().reshape(-1, gic.block_bytes(fmt))
+    return (out, e.cpu().numpy()) if err else out
+
+
+def _manifest():
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        return json.load(f)
+
+
+def _golden_case(name):
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLDEN, "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    for n, fmt, img, kw in mg.cases():
+        if n == name:
+            return fmt, img, kw
+    raise KeyError(name)
+
+
+def _mismatch_report(a, b):
+    bad = np.nonzero((a != b).any(axis=1))[0]
+    return f"{len(bad)} of {len(a)} blocks differ, first {bad[:8].tolist()}"
+
+
+@pytest.mark.parametrize("name", sorted(k for k in _manifest() if not k.startswith("bc7")))
+def test_golden_bcx(gpu, name):
+    fmt, img, kw = _golden_case(name)
+    opts = gic.Options(bc4_channel=kw.get("bc4_channel", 1))
+    out = gpu_encode(fmt, img, opts)
+    ref = np.fromfile(os.path.join(GOLDEN, name + ".bin"), np.uint8).reshape(out.shape)
+    assert np.array_equal(out, ref), _mismatch_report(out, ref)
+
+
+@pytest.mark.parametrize("w,h", [(1, 1), (3, 5), (5, 3), (4, 4), (7, 9), (257, 257), (130, 66)])
+def test_bc1_edges_and_npot(gpu, w, h):
+    img = synth.noise_rgba(w, h, seed=w * 131 + h, alpha=True)
+    out = gpu_encode(gic.FMT_BC1, img)
+    ref = oracle_lib.encode_image(1, img)
+    assert np.array_equal(out, ref), _mismatch_report(out, ref)
+
+
+@pytest.mark.parametrize("channels", [1, 2, 3, 4])
+def test_bc1_bc5_channel_layouts(gpu, channels):
+    img = synth.noise_rgba(48, 40, seed=channels)[..., :channels]
+    for fmt in (1, 5):
+        if fmt == 5 and channels < 2:
+            continue
+        out = gpu_encode(fmt, img)
+        ref = oracle_lib.encode_image(fmt, img)
+        assert np.array_equal(out, ref), (fmt, _mismatch_report(out, ref))
+
+
+def test_bc1_solid_and_transparent_blocks(gpu):
+    img = np.zeros((16, 16, 4), np.uint8)
+    img[:8, :8] = (10, 200, 30, 255)        # solid colour
+    img[:8, 8:] = (0, 0, 0, 0)              # fully transparent
+    img[8:, :8] = (255, 255, 255, 255)      # solid white
+    img[8:, 8:, :3] = 77
+    img[8:, 8:, 3] = np.arange(64).reshape(8, 8) * 4  # alpha ramp across the threshold
+    out = gpu_encode(gic.FMT_BC1, img)
+    assert np.array_equal(out, oracle_lib.encode_image(1, img))
+
+
+def test_bc1_block_api_arbitrary_floats(gpu):
+    """Image_CompressAMDBC1Block / AlphaSingleModeBlock on float inputs that do
+    not come from 8-bit texels (the general block-level contract)."""
+    lib = gic.library()
+    rng = np.random.default_rng(5)
+    for k in range(64):
+        blk = rng.random((16, 4), dtype=np.float32)
+        if k % 4 == 0:
+            blk[:, 3] = 1.0
+        out = np.zeros(8, np.uint8)
+        lib.Image_CompressAMDBC1Block(blk.ctypes.data_as(ctypes.c_void_p), False, False, 1,
+                                      ctypes.c_float(128 / 255.0), out.ctypes.data_as(ctypes.c_void_p))
+        assert out.tobytes() == oracle_lib.bc1_block(blk), k
+        v = rng.random(16, dtype=np.float32)
+        out4 = np.zeros(8, np.uint8)
+        lib.Image_CompressAMDAlphaSingleModeBlock(v.ctypes.data_as(ctypes.c_void_p),
+                                                  out4.ctypes.data_as(ctypes.c_void_p))
+        assert out4.tobytes() == oracle_lib.bc4_block(v), k
+
+
+def test_bc1_refinement_steps_option(gpu):
+    img = synth.g1(64, 64)
+    for steps in (0, 2, 3):
+        out = gpu_encode(gic.FMT_BC1, img, gic.Options(refinement_steps=steps))
+        blocks = [oracle_lib.bc1_block(_block_f32(img, bx, by), steps=steps)
+                  for by in range(16) for bx in range(16)]
+        assert np.array_equal(out, np.frombuffer(b"".join(blocks), np.uint8).reshape(-1, 8)), steps
+
+
+def _block_f32(img, bx, by):
+    return img[by * 4:by * 4 + 4, bx * 4:bx * 4 + 4].reshape(16, 4).astype(np.float32) / np.float32(255.0)
+
+
+def test_row_shards_and_slices_match_full(gpu):
+    stack = np.stack([synth.g1(96, 80, seed=s) for s in range(3)])
+    full = gpu_encode(gic.FMT_BC1, stack).reshape(3, 20, 24, 8)
+    part = gpu_encode(gic.FMT_BC1, stack, first_row=7, num_rows=5).reshape(3, 5, 24, 8)
+    assert np.array_equal(full[:, 7:12], part)
+    ref = oracle_lib.encode_image(1, stack).reshape(3, 20, 24, 8)
+    assert np.array_equal(full, ref)
+
+
+def test_bc4_channel_select(gpu):
+    img = synth.noise_rgba(32, 32, seed=11)
+    for ch in range(4):
+        out = gpu_encode(gic.FMT_BC4, img, gic.Options(bc4_channel=ch))
+        assert np.array_equal(out, oracle_lib.encode_image(4, img, bc4_channel=ch)), ch
+
+
+def test_host_image_api(gpu):
+    """Image_CompressAMDBC1 / BC5 through the reference-compatible host API."""
+    lib = gic.library()
+
+    class Hdr(ctypes.Structure):
+        _fields_ = [("dataSize", ctypes.c_uint64), ("width", ctypes.c_uint32), ("height", ctypes.c_uint32),
+                    ("depth", ctypes.c_uint32), ("slices", ctypes.c_uint32), ("format", ctypes.c_int),
+                    ("flags", ctypes.c_uint32), ("data", ctypes.c_void_p)]
+    lib.Image_CreateNoClear.restype = ctypes.c_void_p
+    lib.Image_CompressAMDBC1.restype = ctypes.c_void_p
+    lib.Image_CompressAMDBC1.argtypes = [ctypes.c_void_p] * 5
+    lib.Image_CompressAMDBC5.restype = ctypes.c_void_p
+    lib.Image_CompressAMDBC5.argtypes = [ctypes.c_void_p] * 3
+    lib.Image_Destroy.argtypes = [ctypes.c_void_p]
+    img = synth.reference_pattern_rgb(257, 257)[..., :3].copy()
+    p = lib.Image_CreateNoClear(257, 257, 1, 1, 5)    # R8G8B8_UNORM
+    ctypes.memmove(Hdr.from_address(p).data, img.ctypes.data, img.nbytes)
+
+    progress = []
+    CB = ctypes.CFUNCTYPE(ctypes.c_bool, ctypes.c_void_p, ctypes.c_float)
+    cb = CB(lambda user, pct: progress.append(pct) or False)
+    d = lib.Image_CompressAMDBC1(p, None, None, ctypes.cast(cb, ctypes.c_void_p), None)
+    assert d
+    hd = Hdr.from_address(d)
+    assert (hd.width, hd.height, hd.format) == (260, 260, 10)
+    got = np.ctypeslib.as_array((ctypes.c_uint8 * hd.dataSize).from_address(hd.data)).reshape(-1, 8)
+    assert np.array_equal(got, oracle_lib.encode_image(1, img))
+    assert len(progress) == 65 and progress[0] == 0.0
+    lib.Image_Destroy(d)
+    # abort via progress callback -> NULL
+    stop = CB(lambda user, pct: pct > 50)
+    assert not lib.Image_CompressAMDBC1(p, None, None, ctypes.cast(stop, ctypes.c_void_p), None)
+    d5 = lib.Image_CompressAMDBC5(p, None, None)
+    h5 = Hdr.from_address(d5)
+    got5 = np.ctypeslib.as_array((ctypes.c_uint8 * h5.dataSize).from_address(h5.data)).reshape(-1, 16)
+    assert np.array_equal(got5, oracle_lib.encode_image(5, img))
+    lib.Image_Destroy(d5)
+    lib.Image_Destroy(p)
+
+
+@pytest.mark.parametrize("fmt,kind", [(1, "g1"), (1, "g0"), (4, "height"), (5, "normal")])
+def test_full_8k_bit_exact(gpu, fmt, kind):
+    """Configs 2 and 3 at full size, every block compared with the oracle."""
+    n = 8192
+    if kind == "g1":
+        img = synth.g1(n, n)
+    elif kind == "g0":
+        img = synth.g0(n, n)
+    elif kind == "height":
+        img = synth.height_field(n, n, seed=1)
+    else:
+        img = synth.normal_map(synth.height_field(n, n, seed=1))
+    opts = gic.Options(bc4_channel=0)
+    out = gpu_encode(fmt, img, opts)
+    ref = oracle_lib.encode_image(fmt, img, bc4_channel=0)
+    assert np.array_equal(out, ref), _mismatch_report(out, ref)

@@ -1,0 +1,90 @@
+"""CPU tests of the oracle (the CPU restatement) against the pinned values.
+
+Pins (see DESIGN.md "Parity pinning"):
+  * BC7 default-quality mode histogram of the first four block
+    rows of the 256x256 G0 gradient, measured on the compiled reference by the
+    survey probe: m1=38, m3=210, m5=8.
+  * tests/golden/*.bin: fixtures produced by tests/golden/make_golden.py.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib
+from gfx_imagecompress_amd import synth
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _modes(blocks):
+    hist = {}
+    for b in blocks:
+        m = 0
+        while m < 8 and not (b[m >> 3] >> (m & 7)) & 1:
+            m += 1
+        hist[m] = hist.get(m, 0) + 1
+    return hist
+
+
+def test_bc7_g0_mode_histogram_matches_reference_probe():
+    out = oracle_lib.encode_image(7, synth.g0(256, 256), first_row=0, num_rows=4)
+    assert _modes(out) == {1: 38, 3: 210, 5: 8}
+
+
+def _load_cases():
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        return json.load(f)
+
+
+def _golden_input(name, entry):
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLDEN, "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    for n, fmt, img, kw in mg.cases():
+        if n == name:
+            return fmt, img, kw
+    raise KeyError(name)
+
+
+@pytest.mark.parametrize("name", sorted(k for k in _load_cases() if not k.startswith("bc7_g")))
+def test_oracle_reproduces_golden(name):
+    entry = _load_cases()[name]
+    fmt, img, kw = _golden_input(name, entry)
+    assert list(img.shape) == entry["shape"]
+    out = oracle_lib.encode_image(fmt, img, **kw)
+    ref = np.fromfile(os.path.join(GOLDEN, name + ".bin"), np.uint8).reshape(out.shape)
+    assert np.array_equal(out, ref), name
+
+
+def test_oracle_thread_pool_is_deterministic():
+    img = synth.g1(64, 48)
+    a = oracle_lib.encode_image(1, img, threads=1)
+    b = oracle_lib.encode_image(1, img, threads=8)
+    assert np.array_equal(a, b)
+
+
+def test_shake_ramp_is_integer_lerp():
+    """amd_shake.cpp:283-286 ramp == exact integer rounding of the linear lerp
+    (this lets the kernels evaluate ramps in integer arithmetic)."""
+    lib = oracle_lib.lib()
+    rng = np.random.default_rng(0)
+    for clog in (2, 3, 4):
+        n = (1 << clog) - 1
+        for bits in (5, 6, 7, 8):
+            for _ in range(400):
+                p1, p2 = rng.integers(0, 1 << bits, 2)
+                e = [(int(p) << (8 - bits)) | (int(p) >> (2 * bits - 8)) for p in (p1, p2)]
+                for i in range(n + 1):
+                    want = e[0] + (2 * i * (e[1] - e[0]) + n) // (2 * n)
+                    assert lib.orc_bc7_shake_ramp(clog, bits, int(p1), int(p2), i) == want
+
+
+def test_bc7_decoder_roundtrip_solid():
+    blk = np.zeros((16, 4), np.float32)
+    blk[:] = np.array([200, 100, 50, 255], np.float32) / 255.0
+    enc, err = oracle_lib.bc7_block(blk)
+    dec = oracle_lib.bc7_decode(np.frombuffer(enc, np.uint8))[0]
+    assert np.abs(dec.astype(int) - np.array([200, 100, 50, 255])).max() <= 1
