@@ -62,7 +62,7 @@ def make_source(fmt, size, rank, device):
     return torch.from_numpy(synth.normal_map(h)[None].copy()).to(device)
 
 
-def cpu_baseline(fmt, src_host, size, gpu_blocks, budget_s):
+def cpu_baseline(fmt, src_host, size, gpu_blocks, budget_s, avail_rows):
     """Oracle on a bounded prefix of block rows; returns (dict, parity_ok)."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -70,8 +70,8 @@ def cpu_baseline(fmt, src_host, size, gpu_blocks, budget_s):
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     threads = max(1, min(threads, os.cpu_count() or 1, 64))
     bx = (size + 3) // 4
-    by = (size + 3) // 4
-    rows = 2 if fmt == 7 else 16
+    by = min((size + 3) // 4, avail_rows)
+    rows = min(by, 2 if fmt == 7 else 16)
     t0 = time.perf_counter()
     out = oracle_lib.encode_image(fmt, src_host, bc4_channel=0, first_row=0, num_rows=rows, threads=threads)
     dt = time.perf_counter() - t0
@@ -85,7 +85,7 @@ def cpu_baseline(fmt, src_host, size, gpu_blocks, budget_s):
             out = oracle_lib.encode_image(fmt, src_host, bc4_channel=0, first_row=0, num_rows=rows, threads=threads)
             dt = time.perf_counter() - t0
     px = rows * 4 * size
-    gpu_rows = gpu_blocks.reshape(by, bx, -1)[:rows].reshape(out.shape)
+    gpu_rows = gpu_blocks.reshape(-1, bx, out.shape[1])[:rows].reshape(out.shape)
     parity = bool(np.array_equal(gpu_rows, out))
     mism = int((gpu_rows != out).any(axis=1).sum())
     res = {"value": round(px / dt / 1e6, 4), "unit": "Mpixels/s", "cores": threads, "kind": "port",
@@ -176,7 +176,7 @@ def main():
     if rank == 0 and not args.no_cpu:
         host = src.cpu().numpy()[0]
         torch.cuda.synchronize(dev)
-        cpu, parity, mism = cpu_baseline(fmt, host, size, dst.cpu().numpy(), args.cpu_seconds)
+        cpu, parity, mism = cpu_baseline(fmt, host, size, dst.cpu().numpy(), args.cpu_seconds, rows)
         cpu["gpu_parity"] = "bit-exact" if parity else f"{mism} blocks differ"
 
     if rank == 0:
