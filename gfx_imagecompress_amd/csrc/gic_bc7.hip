@@ -77,16 +77,17 @@ struct BlockMeta {
 };
 
 struct ShakeResult {
-    double err;
-    uint64_t idx;          // per-texel index, 4 bits, texel order
+    double err[3];         // per-subset shake error (summed in subset order by k_select)
+    uint64_t idx[3];       // per-subset texel indices, 4 bits per texel, texel order
     uint8_t ep[3][2][4];   // endpoint codes incl. parity bit (LSB) per subset
     uint32_t part;
     uint32_t pad;
 };
 
 struct DualResult {
-    double err;
-    uint8_t block[16];
+    double err[2];         // colour, alpha (alpha divided by 3 when combined)
+    uint64_t idx[2];       // 16 indices each, 4 bits per texel
+    uint8_t ep[2][2][4];   // endpoint codes [half][endpoint][channel]
 };
 
 struct Workspace {
@@ -96,6 +97,7 @@ struct Workspace {
     uint64_t *qidx;        // [n][273]
     ShakeResult *shk;      // [n][6][8]
     DualResult *dual;      // [n][12]
+    uint64_t *dqidx;       // [n][12][2] optQuantAnD_d indices of the dual-index candidates
 };
 
 __device__ __forceinline__ int expand_code(int bits, int v) { return (v << (8 - bits)) | (v >> (2 * bits - 8)); }
@@ -422,10 +424,10 @@ __device__ __forceinline__ double sp_err(const SpEntry *sp, int c, int b, int v,
     return e == 0xffffffffu ? 1.7976931348623157e308 : (double)e;
 }
 
-// quant_single_point_d, amd_shake.cpp:546-701.  Returns the error; when
-// `data` is given (not all-same path) the total error against it is returned.
-__device__ double single_point(const SpEntry *sp, const double point[4], int n, int *index, int epo1[2][4],
-                               int last, const int *bits, int type, int dim, const double (*data)[4])
+// quant_single_point_d, amd_shake.cpp:546-701: best (cluster, endpoint pair)
+// for one point; returns err1 (per point) and the cluster index in idx_out.
+__device__ double single_point_core(const SpEntry *sp, const double point[4], int &idx_out, int epo1[2][4],
+                                    int last, const int *bits, int type, int dim)
 {
     double err0 = 1.7976931348623157e308, err1 = 1.7976931348623157e308;
     int idx = 0, idx1 = 0, epo0[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
@@ -494,9 +496,20 @@ __device__ double single_point(const SpEntry *sp, const double point[4], int n, 
         }
         if (err1 == 0) break;
     }
+    idx_out = idx1;
+    return err1;
+}
+
+// Returns err1 * n, or, when `data` is given (not all-same path), the
+// totalError_d of the reconstruction against it.
+__device__ double single_point(const SpEntry *sp, const double point[4], int n, int *index, int epo1[2][4],
+                               int last, const int *bits, int type, int dim, const double (*data)[4])
+{
+    int idx1;
+    const double err1 = single_point_core(sp, point, idx1, epo1, last, bits, type, dim);
+    const int clog = clog_of(last);
     for (int i = 0; i < n; ++i) index[i] = idx1;
     if (!data) return err1 * n;
-    // totalError_d against the single reconstructed point
     double t = 0;
     for (int i = 0; i < n; ++i)
         for (int j = 0; j < dim; ++j) {
@@ -1061,7 +1074,8 @@ __global__ void __launch_bounds__(256) k_quant(Params p, Workspace ws)
     ws.qidx[(size_t)b * kQuantTasks + task] = tidx;
 }
 
-// one subset of CompressSingleIndexBlock's shake loop (amd_bc7_body.cpp:721-805)
+// one subset of CompressSingleIndexBlock's shake loop (amd_bc7_body.cpp:721-805),
+// per-lane f64 path (blocks with fractional texels)
 template <typename T>
 __device__ double shake_subset(const SpEntry *sp, const double sub[][4], const T *tsub, int n, int *idx, int epo[2][4],
                                bool corners_too, int shake, int last, const int *bits, int parity, int dim)
@@ -1082,8 +1096,60 @@ __device__ double shake_subset(const SpEntry *sp, const double sub[][4], const T
     return e1;
 }
 
-// K2: shaking of the 8 best partitions of a single-index mode
-// (CompressSingleIndexBlock :644-844)
+// Shake parameters of a single-index mode (amd_bc7_body.cpp:654-706, quality 1)
+struct ShakeCfg {
+    int dim, parity, last, shake, bits[4];
+};
+
+__device__ ShakeCfg shake_cfg(int mode)
+{
+    const ModeInfo &mi = kModes[mode];
+    ShakeCfg c;
+    c.dim = mi.enc == ENC_NO_ALPHA ? 3 : 4;
+    c.parity = mi.pbit == 0 ? PAR_CART : mi.pbit == 1 ? PAR_SAME : PAR_BCC;
+    int cbits[4];
+    if (mi.enc == ENC_NO_ALPHA) {
+        cbits[0] = cbits[1] = cbits[2] = mi.vector_bits / 3;
+        cbits[3] = 0;
+    } else {
+        cbits[0] = cbits[1] = cbits[2] = cbits[3] = mi.vector_bits / 4;
+    }
+    c.bits[0] = cbits[0] + (c.parity ? 1 : 0);
+    c.bits[1] = cbits[1] + (c.parity ? 1 : 0);
+    c.bits[2] = cbits[2] + (c.parity ? 1 : 0);
+    c.bits[3] = 0;
+    for (int i = 0; i < c.dim; ++i) c.bits[3] += cbits[i];
+    c.bits[3] *= 2;
+    if (c.parity == PAR_BCC)
+        c.bits[3] += 2;
+    else if (c.parity == PAR_SAME)
+        c.bits[3] += 1;
+    int shake = 8 - (int)floor(1.5 * mi.ib0);
+    shake = shake < 6 ? shake : 6;   // quality 1: floor(shake * 1 + 0.5) = shake
+    shake = shake > 2 ? shake : 2;
+    if (c.parity == PAR_SAME || c.parity == PAR_BCC) shake += 2;
+    c.shake = shake;
+    c.last = (1 << mi.ib0) - 1;
+    return c;
+}
+
+// partition whose stable rank is `rank` (sortProjection, amd_bc7_3dquant_vpc.cpp:138-150)
+__device__ int partition_of_rank(const double *qe, int nparts, int rank)
+{
+    for (int c = 0; c < nparts; ++c) {
+        const double v = qe[c];
+        int rk = 0;
+        for (int o = 0; o < nparts; ++o) {
+            const double w = qe[o];
+            rk += (w - v < 0 || (!(w - v > 0) && !(w - v < 0) && o < c)) ? 1 : 0;
+        }
+        if (rk == rank) return c;
+    }
+    return 0;
+}
+
+// K2 (f64 lanes): shaking of the 8 best partitions of a single-index mode
+// for blocks with fractional texels (CompressSingleIndexBlock :644-844)
 __global__ void __launch_bounds__(256) k_shake(Params p, Workspace ws, const SpEntry *__restrict__ sp)
 {
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1093,91 +1159,219 @@ __global__ void __launch_bounds__(256) k_shake(Params p, Workspace ws, const SpE
     const int slot = (int)(r / kShakeRanks), rank = (int)(r % kShakeRanks);
     const int mode = kSlotMode[slot];
     const BlockMeta meta = ws.meta[b];
-    if (!(meta.valid & (1u << mode)) || (meta.flags & 1u)) return;
+    if (!(meta.valid & (1u << mode)) || (meta.flags & 3u)) return;   // integral blocks: k_shake_wave
     const ModeInfo &mi = kModes[mode];
     const int nparts = 1 << mi.part_bits;
     const int attempts = nparts < 8 ? nparts : 8;
     if (rank >= attempts) return;
-    // partition whose stable rank is `rank` (sortProjection, amd_bc7_3dquant_vpc.cpp:138-150)
-    const double *qe = ws.qerr + (size_t)b * kQuantTasks + kSlotBase[slot];
-    int part = 0;
-    for (int c = 0; c < nparts; ++c) {
-        const double v = qe[c];
-        int rk = 0;
-        for (int o = 0; o < nparts; ++o) {
-            const double w = qe[o];
-            rk += (w - v < 0 || (!(w - v > 0) && !(w - v < 0) && o < c)) ? 1 : 0;
-        }
-        if (rk == rank) {
-            part = c;
-            break;
-        }
-    }
+    const int part = partition_of_rank(ws.qerr + (size_t)b * kQuantTasks + kSlotBase[slot], nparts, rank);
     const uint64_t qidx = ws.qidx[(size_t)b * kQuantTasks + kSlotBase[slot] + part];
-    const int dim = mi.enc == ENC_NO_ALPHA ? 3 : 4;
-    int cbits[4];
-    int parity = mi.pbit == 0 ? PAR_CART : mi.pbit == 1 ? PAR_SAME : PAR_BCC;
-    if (mi.enc == ENC_NO_ALPHA) {
-        cbits[0] = cbits[1] = cbits[2] = mi.vector_bits / 3;
-        cbits[3] = 0;
-    } else {
-        cbits[0] = cbits[1] = cbits[2] = cbits[3] = mi.vector_bits / 4;
-    }
-    int bits[4] = {0, 0, 0, 0};
-    bits[0] = cbits[0] + (parity ? 1 : 0);
-    bits[1] = cbits[1] + (parity ? 1 : 0);
-    bits[2] = cbits[2] + (parity ? 1 : 0);
-    for (int i = 0; i < dim; ++i) bits[3] += cbits[i];
-    bits[3] *= 2;
-    if (parity == PAR_BCC)
-        bits[3] += 2;
-    else if (parity == PAR_SAME)
-        bits[3] += 1;
-    int shake = 8 - (int)floor(1.5 * mi.ib0);
-    shake = shake < 6 ? shake : 6;   // quality 1: floor(shake * 1 + 0.5) = shake
-    shake = shake > 2 ? shake : 2;
-    if (parity == PAR_SAME || parity == PAR_BCC) shake += 2;
-    const int last = (1 << mi.ib0) - 1;
+    const ShakeCfg cfg = shake_cfg(mode);
     const float *tex = ws.tex + (size_t)b * 64;
-    ShakeResult res;
-    res.err = 0;
-    res.idx = 0;
+    ShakeResult &res = ws.shk[((size_t)b * kShakeSlots + slot) * kShakeRanks + rank];
     res.part = (uint32_t)part;
-    res.pad = 0;
-    for (int s = 0; s < 3; ++s)
-        for (int k = 0; k < 2; ++k)
-            for (int c = 0; c < 4; ++c) res.ep[s][k][c] = 0;
-    const bool corners_too = !(meta.max_range > 255.0) && dim == 3;   // m_shakerRangeThreshold = 255
-    double err = 0;
+    const bool corners_too = !(meta.max_range > 255.0) && cfg.dim == 3;   // m_shakerRangeThreshold = 255
     for (int s = 0; s < mi.subsets; ++s) {
         double sub[16][4];
-        int isub[16 * 4], tex_of[16], n = 0, idx[16];
+        int tex_of[16], n = 0, idx[16];
         for (int i = 0; i < 16; ++i)
             if ((int)shape_of(mi.subsets, part, i) == s) {
-                for (int j = 0; j < dim; ++j) {
-                    sub[n][j] = (double)tex[i * 4 + j];
-                    isub[n * 4 + j] = (int)tex[i * 4 + j];
-                }
+                for (int j = 0; j < cfg.dim; ++j) sub[n][j] = (double)tex[i * 4 + j];
                 idx[n] = (int)((qidx >> (4 * i)) & 15u);
                 tex_of[n++] = i;
             }
-        if (!n) continue;
         int epo[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-        if (meta.flags & 2u)
-            err += shake_subset<int>(sp, sub, isub, n, idx, epo, corners_too, shake, last, bits, parity, dim);
-        else
-            err += shake_subset<double>(sp, sub, &sub[0][0], n, idx, epo, corners_too, shake, last, bits, parity, dim);
-        for (int k = 0; k < n; ++k) res.idx |= (uint64_t)(idx[k] & 15) << (4 * tex_of[k]);
-        for (int k = 0; k < dim; ++k) {
+        const double e = shake_subset<double>(sp, sub, &sub[0][0], n, idx, epo, corners_too, cfg.shake, cfg.last,
+                                              cfg.bits, cfg.parity, cfg.dim);
+        uint64_t ti = 0;
+        for (int k = 0; k < n; ++k) ti |= (uint64_t)(idx[k] & 15) << (4 * tex_of[k]);
+        res.err[s] = e;
+        res.idx[s] = ti;
+        for (int k = 0; k < 4; ++k) {
             res.ep[s][0][k] = (uint8_t)epo[0][k];
             res.ep[s][1][k] = (uint8_t)epo[1][k];
         }
     }
-    res.err = err;
-    ws.shk[((size_t)b * kShakeSlots + slot) * kShakeRanks + rank] = res;
 }
 
-// K3: dual-index modes 4/5 (CompressDualIndexBlock, amd_bc7_body.cpp:1059-1278)
+#include "bc7_wave.inc"
+
+// problem id -> (slot, rank, subset) for the wave shaker: modes 0..3 (80
+// problems), mode 6 (1), mode 7 (16)
+constexpr int kWaveProblems = 97;
+__device__ __forceinline__ bool wave_problem(int id, int &slot, int &rank, int &subset)
+{
+    const int sub_count[4] = {3, 2, 3, 2};
+    int base = 0;
+    for (int sl = 0; sl < 4; ++sl) {
+        const int cnt = 8 * sub_count[sl];
+        if (id < base + cnt) {
+            slot = sl;
+            rank = (id - base) / sub_count[sl];
+            subset = (id - base) % sub_count[sl];
+            return true;
+        }
+        base += cnt;
+    }
+    if (id == 80) {
+        slot = 4;
+        rank = 0;
+        subset = 0;
+        return true;
+    }
+    slot = 5;
+    rank = (id - 81) / 2;
+    subset = (id - 81) % 2;
+    return id < kWaveProblems;
+}
+
+// K2 (waves): one wavefront per (block, mode, rank, subset) shake problem of
+// an integral block
+__global__ void __launch_bounds__(256) k_shake_wave(Params p, Workspace ws, const SpEntry *__restrict__ sp)
+{
+    const uint32_t wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t b = wid / kWaveProblems;
+    if (b >= p.n) return;
+    int slot, rank, subset;
+    if (!wave_problem((int)(wid % kWaveProblems), slot, rank, subset)) return;
+    const int mode = kSlotMode[slot];
+    const BlockMeta meta = ws.meta[b];
+    if (!(meta.valid & (1u << mode)) || (meta.flags & 3u) != 2u) return;
+    const ModeInfo &mi = kModes[mode];
+    const int nparts = 1 << mi.part_bits;
+    const int attempts = nparts < 8 ? nparts : 8;
+    if (rank >= attempts) return;
+    const int part = partition_of_rank(ws.qerr + (size_t)b * kQuantTasks + kSlotBase[slot], nparts, rank);
+    const uint64_t qidx = ws.qidx[(size_t)b * kQuantTasks + kSlotBase[slot] + part];
+    const ShakeCfg cfg = shake_cfg(mode);
+    const float *tex = ws.tex + (size_t)b * 64;
+    // gather the subset: lane L < n holds the L-th texel of the subset
+    const int ln = wv::lane();
+    uint32_t mask = 0;
+    for (int t = 0; t < 16; ++t) mask |= ((int)shape_of(mi.subsets, part, t) == subset ? 1u : 0u) << t;
+    const int n = __popc(mask);
+    int src = 0;
+    {
+        int cnt = 0;
+        for (int t = 0; t < 16; ++t)
+            if ((mask >> t) & 1u) {
+                if (cnt == ln) src = t;
+                cnt++;
+            }
+    }
+    wv::Texels T;
+    T.n = n;
+    T.dim = cfg.dim;
+    T.live = ln < n;
+    for (int j = 0; j < 4; ++j) T.d[j] = (T.live && j < cfg.dim) ? (int)tex[src * 4 + j] : 0;
+    int idx = T.live ? (int)((qidx >> (4 * src)) & 15u) : 0;
+    int epo[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+    const bool corners_too = !(meta.max_range > 255.0) && cfg.dim == 3;
+    const int nc = cfg.last + 1;
+    double e;
+    if (nc == 4)
+        e = wv::subset_shake<4>(sp, T, idx, epo, corners_too, cfg.shake, cfg.last, cfg.bits, cfg.parity);
+    else if (nc == 8)
+        e = wv::subset_shake<8>(sp, T, idx, epo, corners_too, cfg.shake, cfg.last, cfg.bits, cfg.parity);
+    else
+        e = wv::subset_shake<16>(sp, T, idx, epo, corners_too, cfg.shake, cfg.last, cfg.bits, cfg.parity);
+    unsigned long long ti = T.live ? (unsigned long long)(idx & 15) << (4 * src) : 0ull;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ti |= __shfl_xor(ti, o);
+    if (ln == 0) {
+        ShakeResult &res = ws.shk[((size_t)b * kShakeSlots + slot) * kShakeRanks + rank];
+        if (subset == 0) res.part = (uint32_t)part;
+        res.err[subset] = e;
+        res.idx[subset] = ti;
+        for (int k = 0; k < 4; ++k) {
+            res.ep[subset][0][k] = (uint8_t)epo[0][k];
+            res.ep[subset][1][k] = (uint8_t)epo[1][k];
+        }
+    }
+}
+
+// K3a: dual-index quantisation (CompressDualIndexBlock :1084-1152): optQuantAnD_d
+// for the colour and the replicated-alpha halves of each (rotation, selection)
+__global__ void __launch_bounds__(256) k_dual_quant(Params p, Workspace ws)
+{
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t b = gid / (kDualTasks * 2), r = gid % (kDualTasks * 2);
+    if (b >= p.n) return;
+    const uint32_t task = r >> 1, half = r & 1;
+    const int mode = task < 8 ? 4 : 5;
+    const int rot = task < 8 ? (int)(task >> 1) : (int)(task - 8);
+    const int sel = task < 8 ? (int)(task & 1) : 0;
+    const BlockMeta meta = ws.meta[b];
+    if (!(meta.valid & (1u << mode)) || (meta.flags & 1u)) return;
+    const ModeInfo &mi = kModes[mode];
+    const int ibs[2] = {mi.ib0, mi.ib1};
+    const float *tex = ws.tex + (size_t)b * 64;
+    double blk[16][4];
+    for (int i = 0; i < 16; ++i) {
+        for (int j = 0; j < 3; ++j) blk[i][j] = (double)tex[i * 4 + kRot[rot][half ? 0 : j + 1]];
+        blk[i][3] = 0.0;
+    }
+    int idx[16];
+    opt_quant(blk, 16, 1 << ibs[half ? 1 ^ sel : sel], idx, 3);
+    uint64_t ti = 0;
+    for (int k = 0; k < 16; ++k) ti |= (uint64_t)(idx[k] & 15) << (4 * k);
+    ws.dqidx[((size_t)b * kDualTasks + task) * 2 + half] = ti;
+}
+
+// K3b (waves): shakers of one half of a dual-index candidate
+// (CompressDualIndexBlock :1158-1254); integral blocks
+__global__ void __launch_bounds__(256) k_dual_wave(Params p, Workspace ws, const SpEntry *__restrict__ sp)
+{
+    const uint32_t wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t b = wid / (kDualTasks * 2), r = wid % (kDualTasks * 2);
+    if (b >= p.n) return;
+    const uint32_t task = r >> 1, half = r & 1;
+    const int mode = task < 8 ? 4 : 5;
+    const int rot = task < 8 ? (int)(task >> 1) : (int)(task - 8);
+    const int sel = task < 8 ? (int)(task & 1) : 0;
+    const BlockMeta meta = ws.meta[b];
+    if (!(meta.valid & (1u << mode)) || (meta.flags & 3u) != 2u) return;
+    const ModeInfo &mi = kModes[mode];
+    const int ibs[2] = {mi.ib0, mi.ib1};
+    const float *tex = ws.tex + (size_t)b * 64;
+    const int ln = wv::lane();
+    wv::Texels T;
+    T.n = 16;
+    T.dim = 3;
+    T.live = ln < 16;
+    for (int j = 0; j < 3; ++j) T.d[j] = T.live ? (int)tex[ln * 4 + kRot[rot][half ? 0 : j + 1]] : 0;
+    T.d[3] = 0;
+    const uint64_t qi = ws.dqidx[((size_t)b * kDualTasks + task) * 2 + half];
+    int idx = T.live ? (int)((qi >> (4 * ln)) & 15u) : 0;
+    const int ib = half ? ibs[1 ^ sel] : ibs[sel];
+    const int last = (1 << ib) - 1;
+    const int cb = half ? mi.scalar_bits : mi.vector_bits / 3;
+    const int bits[4] = {cb, cb, cb, half ? 6 * cb : 2 * 3 * cb};
+    int epo[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+    const bool corners_too = !(meta.max_range > 255.0);
+    double e;
+    if (last == 3) {
+        if (corners_too) wv::corners<4>(sp, T, idx, epo, last, bits, PAR_CART);   // Q9: error ignored
+        e = wv::window<4>(sp, T, idx, epo, 6, last, bits[3]);
+    } else {
+        if (corners_too) wv::corners<8>(sp, T, idx, epo, last, bits, PAR_CART);
+        e = wv::window<8>(sp, T, idx, epo, 6, last, bits[3]);
+    }
+    unsigned long long ti = T.live ? (unsigned long long)(idx & 15) << (4 * ln) : 0ull;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ti |= __shfl_xor(ti, o);
+    if (ln == 0) {
+        DualResult &res = ws.dual[(size_t)b * kDualTasks + task];
+        res.err[half] = e;
+        res.idx[half] = ti;
+        for (int k = 0; k < 4; ++k) {
+            res.ep[half][0][k] = (uint8_t)epo[0][k];
+            res.ep[half][1][k] = (uint8_t)epo[1][k];
+        }
+    }
+}
+
+// K3 (f64 lanes): dual-index candidates of blocks with fractional texels
 __global__ void __launch_bounds__(256) k_dual(Params p, Workspace ws, const SpEntry *__restrict__ sp)
 {
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1187,24 +1381,23 @@ __global__ void __launch_bounds__(256) k_dual(Params p, Workspace ws, const SpEn
     const int rot = task < 8 ? (int)(task >> 1) : (int)(task - 8);
     const int sel = task < 8 ? (int)(task & 1) : 0;
     const BlockMeta meta = ws.meta[b];
-    if (!(meta.valid & (1u << mode)) || (meta.flags & 1u)) return;
+    if (!(meta.valid & (1u << mode)) || (meta.flags & 3u)) return;
     const ModeInfo &mi = kModes[mode];
     const int ibs[2] = {mi.ib0, mi.ib1};
     const float *tex = ws.tex + (size_t)b * 64;
     double cb[16][4], ab[16][4];
-    int icb[64], iab[64];
     for (int i = 0; i < 16; ++i) {
         for (int j = 0; j < 3; ++j) {
             cb[i][j] = (double)tex[i * 4 + kRot[rot][j + 1]];
-            icb[i * 4 + j] = (int)tex[i * 4 + kRot[rot][j + 1]];
             ab[i][j] = (double)tex[i * 4 + kRot[rot][0]];
-            iab[i * 4 + j] = (int)tex[i * 4 + kRot[rot][0]];
         }
         cb[i][3] = ab[i][3] = 0.0;
     }
     int idx[2][16];
-    opt_quant(cb, 16, 1 << ibs[sel], idx[0], 3);
-    opt_quant(ab, 16, 1 << ibs[1 ^ sel], idx[1], 3);
+    for (int h = 0; h < 2; ++h) {
+        const uint64_t qi = ws.dqidx[((size_t)b * kDualTasks + task) * 2 + h];
+        for (int k = 0; k < 16; ++k) idx[h][k] = (int)((qi >> (4 * k)) & 15u);
+    }
     const int shake = 6;   // max(2, min((uint32_t)(6 * 1.0), 6))
     const int cbits = mi.vector_bits / 3, abits = mi.scalar_bits;
     const int bits0[4] = {cbits, cbits, cbits, 2 * 3 * cbits};
@@ -1212,29 +1405,22 @@ __global__ void __launch_bounds__(256) k_dual(Params p, Workspace ws, const SpEn
     const int last0 = (1 << ibs[sel]) - 1, last1 = (1 << ibs[1 ^ sel]) - 1;
     int epo[2][2][4] = {{{0, 0, 0, 0}, {0, 0, 0, 0}}, {{0, 0, 0, 0}, {0, 0, 0, 0}}};
     const bool corners_too = !(meta.max_range > 255.0);
-    double overall = 0;
-    if (meta.flags & 2u) {
-        if (corners_too) shake_corners<int>(sp, cb, icb, 16, idx[0], epo[0], last0, bits0, PAR_CART);   // Q9
-        overall += shake_window<int>(sp, cb, icb, 16, idx[0], epo[0], shake, last0, bits0[3], 3);
-        if (corners_too) shake_corners<int>(sp, ab, iab, 16, idx[1], epo[1], last1, bits1, PAR_CART);
-        overall += shake_window<int>(sp, ab, iab, 16, idx[1], epo[1], shake, last1, bits1[3], 3) / 3.;
-    } else {
-        if (corners_too) shake_corners<double>(sp, cb, &cb[0][0], 16, idx[0], epo[0], last0, bits0, PAR_CART);
-        overall += shake_window<double>(sp, cb, &cb[0][0], 16, idx[0], epo[0], shake, last0, bits0[3], 3);
-        if (corners_too) shake_corners<double>(sp, ab, &ab[0][0], 16, idx[1], epo[1], last1, bits1, PAR_CART);
-        overall += shake_window<double>(sp, ab, &ab[0][0], 16, idx[1], epo[1], shake, last1, bits1[3], 3) / 3.;
+    if (corners_too) shake_corners<double>(sp, cb, &cb[0][0], 16, idx[0], epo[0], last0, bits0, PAR_CART);   // Q9
+    const double ec = shake_window<double>(sp, cb, &cb[0][0], 16, idx[0], epo[0], shake, last0, bits0[3], 3);
+    if (corners_too) shake_corners<double>(sp, ab, &ab[0][0], 16, idx[1], epo[1], last1, bits1, PAR_CART);
+    const double ea = shake_window<double>(sp, ab, &ab[0][0], 16, idx[1], epo[1], shake, last1, bits1[3], 3);
+    DualResult &res = ws.dual[(size_t)b * kDualTasks + task];
+    res.err[0] = ec;
+    res.err[1] = ea;
+    for (int h = 0; h < 2; ++h) {
+        uint64_t ti = 0;
+        for (int k = 0; k < 16; ++k) ti |= (uint64_t)(idx[h][k] & 15) << (4 * k);
+        res.idx[h] = ti;
+        for (int k = 0; k < 4; ++k) {
+            res.ep[h][0][k] = (uint8_t)epo[h][0][k];
+            res.ep[h][1][k] = (uint8_t)epo[h][1][k];
+        }
     }
-    DualResult res;
-    uint32_t w[4];
-    pack_dual(mode, sel, rot, epo, idx, w);
-    res.err = overall;
-    for (int k = 0; k < 4; ++k) {
-        res.block[4 * k + 0] = (uint8_t)w[k];
-        res.block[4 * k + 1] = (uint8_t)(w[k] >> 8);
-        res.block[4 * k + 2] = (uint8_t)(w[k] >> 16);
-        res.block[4 * k + 3] = (uint8_t)(w[k] >> 24);
-    }
-    ws.dual[(size_t)b * kDualTasks + task] = res;
 }
 
 // K4: mode selection in the reference's visiting order (CompressBlock :1400-1447)
@@ -1259,29 +1445,43 @@ __global__ void __launch_bounds__(256) k_select(Params p, Workspace ws, uint4 *_
         uint32_t w[4];
         if (m == 4 || m == 5) {
             const int t0 = m == 4 ? 0 : 8, nt = m == 4 ? 8 : 4;
-            int bi = -1;
+            int bi = 0;
             double be = 1.7976931348623157e308;
             for (int t = 0; t < nt; ++t) {
-                const double v = ws.dual[(size_t)b * kDualTasks + t0 + t].err;
+                const DualResult &dr = ws.dual[(size_t)b * kDualTasks + t0 + t];
+                double v = 0;
+                v += dr.err[0];
+                v += dr.err[1] / 3.;
                 if (v < be) {
                     be = v;
                     bi = t;
                 }
             }
             e = be;
-            if (bi < 0) bi = 0;
-            const uint8_t *blk = ws.dual[(size_t)b * kDualTasks + t0 + bi].block;
-            for (int q = 0; q < 4; ++q)
-                w[q] = (uint32_t)blk[4 * q] | ((uint32_t)blk[4 * q + 1] << 8) | ((uint32_t)blk[4 * q + 2] << 16) |
-                       ((uint32_t)blk[4 * q + 3] << 24);
+            const DualResult &dr = ws.dual[(size_t)b * kDualTasks + t0 + bi];
+            int ep[2][2][4], idx[2][16];
+            for (int h = 0; h < 2; ++h) {
+                for (int q = 0; q < 4; ++q) {
+                    ep[h][0][q] = dr.ep[h][0][q];
+                    ep[h][1][q] = dr.ep[h][1][q];
+                }
+                for (int q = 0; q < 16; ++q) idx[h][q] = (int)((dr.idx[h] >> (4 * q)) & 15u);
+            }
+            const int task = t0 + bi;
+            const int rot = task < 8 ? (task >> 1) : (task - 8);
+            const int sel = task < 8 ? (task & 1) : 0;
+            pack_dual(m, sel, rot, ep, idx, w);
         } else {
             const int slot = m <= 3 ? m : (m == 6 ? 4 : 5);
             const int nparts = 1 << kModes[m].part_bits;
             const int attempts = nparts < 8 ? nparts : 8;
+            const int ns = kModes[m].subsets;
             int bi = 0;
             double be = 1.7976931348623157e308;
             for (int r = 0; r < attempts; ++r) {
-                const double v = ws.shk[((size_t)b * kShakeSlots + slot) * kShakeRanks + r].err;
+                const ShakeResult &sr = ws.shk[((size_t)b * kShakeSlots + slot) * kShakeRanks + r];
+                double v = 0;
+                for (int s = 0; s < ns; ++s) v += sr.err[s];
                 if (v < be) {
                     be = v;
                     bi = r;
@@ -1289,7 +1489,8 @@ __global__ void __launch_bounds__(256) k_select(Params p, Workspace ws, uint4 *_
             }
             e = be;
             const ShakeResult &sr = ws.shk[((size_t)b * kShakeSlots + slot) * kShakeRanks + bi];
-            pack_single(m, (int)sr.part, sr.ep, sr.idx, w);
+            const uint64_t tidx = sr.idx[0] | (ns > 1 ? sr.idx[1] : 0ull) | (ns > 2 ? sr.idx[2] : 0ull);
+            pack_single(m, (int)sr.part, sr.ep, tidx, w);
         }
         if (e < best) {
             best = e;
@@ -1397,7 +1598,7 @@ static hipError_t get_state(uint32_t chunk, DeviceState *&out)
         const size_t sz = align_up(n * 64 * sizeof(float)) + align_up(n * sizeof(BlockMeta)) +
                           align_up(n * kQuantTasks * sizeof(double)) + align_up(n * kQuantTasks * sizeof(uint64_t)) +
                           align_up(n * kShakeSlots * kShakeRanks * sizeof(ShakeResult)) +
-                          align_up(n * kDualTasks * sizeof(DualResult));
+                          align_up(n * kDualTasks * sizeof(DualResult)) + align_up(n * kDualTasks * 2 * sizeof(uint64_t));
         e = hipMalloc(&st.ws_mem, sz);
         if (e != hipSuccess) return e;
         char *p = (char *)st.ws_mem;
@@ -1412,6 +1613,8 @@ static hipError_t get_state(uint32_t chunk, DeviceState *&out)
         st.ws.shk = (ShakeResult *)p;
         p += align_up(n * kShakeSlots * kShakeRanks * sizeof(ShakeResult));
         st.ws.dual = (DualResult *)p;
+        p += align_up(n * kDualTasks * sizeof(DualResult));
+        st.ws.dqidx = (uint64_t *)p;
         st.ws_blocks = chunk;
     }
     out = &st;
@@ -1444,8 +1647,14 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
         hipLaunchKernelGGL(k_quant, dim3((uint32_t)((nq + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws);
         const uint64_t ns = (uint64_t)p.n * kShakeSlots * kShakeRanks;
         hipLaunchKernelGGL(k_shake, dim3((uint32_t)((ns + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
+        const uint64_t nw = (uint64_t)p.n * kWaveProblems * 64;
+        hipLaunchKernelGGL(k_shake_wave, dim3((uint32_t)((nw + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
+        const uint64_t ndq = (uint64_t)p.n * kDualTasks * 2;
+        hipLaunchKernelGGL(k_dual_quant, dim3((uint32_t)((ndq + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws);
         const uint64_t nd = (uint64_t)p.n * kDualTasks;
         hipLaunchKernelGGL(k_dual, dim3((uint32_t)((nd + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
+        const uint64_t ndw = (uint64_t)p.n * kDualTasks * 2 * 64;
+        hipLaunchKernelGGL(k_dual_wave, dim3((uint32_t)((ndw + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
         hipLaunchKernelGGL(k_select, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, p, st->ws, (uint4 *)dst, err);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
