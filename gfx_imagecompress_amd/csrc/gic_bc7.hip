@@ -1196,44 +1196,45 @@ __global__ void __launch_bounds__(256) k_shake(Params p, Workspace ws, const SpE
 
 #include "bc7_wave.inc"
 
-// problem id -> (slot, rank, subset) for the wave shaker: modes 0..3 (80
-// problems), mode 6 (1), mode 7 (16)
-constexpr int kWaveProblems = 97;
-__device__ __forceinline__ bool wave_problem(int id, int &slot, int &rank, int &subset)
+// Wave shaker problems, one kernel per cluster count NC:
+//   NC = 8 : modes 0, 1 (slots 0, 1)      -> 8 ranks x (3 + 2) subsets = 40
+//   NC = 4 : modes 2, 3, 7 (slots 2, 3, 5) -> 8 x (3 + 2 + 2)          = 56
+//   NC = 16: mode 6 (slot 4)               -> 1
+template <int NC> struct WaveSet;
+template <> struct WaveSet<8> { static constexpr int count = 40; };
+template <> struct WaveSet<4> { static constexpr int count = 56; };
+template <> struct WaveSet<16> { static constexpr int count = 1; };
+
+template <int NC>
+__device__ __forceinline__ void wave_problem(int id, int &slot, int &rank, int &subset)
 {
-    const int sub_count[4] = {3, 2, 3, 2};
+    const int nsl = NC == 8 ? 2 : (NC == 4 ? 3 : 1);
+    const int slots8[2] = {0, 1}, slots4[3] = {2, 3, 5};
     int base = 0;
-    for (int sl = 0; sl < 4; ++sl) {
-        const int cnt = 8 * sub_count[sl];
-        if (id < base + cnt) {
+    for (int k = 0; k < nsl; ++k) {
+        const int sl = NC == 8 ? slots8[k] : (NC == 4 ? slots4[k] : 4);
+        const int ns = kModes[kSlotMode[sl]].subsets;
+        const int cnt = (sl == 4 ? 1 : 8) * ns;
+        if (id < base + cnt || k == nsl - 1) {
             slot = sl;
-            rank = (id - base) / sub_count[sl];
-            subset = (id - base) % sub_count[sl];
-            return true;
+            rank = (id - base) / ns;
+            subset = (id - base) % ns;
+            return;
         }
         base += cnt;
     }
-    if (id == 80) {
-        slot = 4;
-        rank = 0;
-        subset = 0;
-        return true;
-    }
-    slot = 5;
-    rank = (id - 81) / 2;
-    subset = (id - 81) % 2;
-    return id < kWaveProblems;
 }
 
 // K2 (waves): one wavefront per (block, mode, rank, subset) shake problem of
 // an integral block
+template <int NC>
 __global__ void __launch_bounds__(256) k_shake_wave(Params p, Workspace ws, const SpEntry *__restrict__ sp)
 {
     const uint32_t wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint32_t b = wid / kWaveProblems;
+    const uint32_t b = wid / WaveSet<NC>::count;
     if (b >= p.n) return;
     int slot, rank, subset;
-    if (!wave_problem((int)(wid % kWaveProblems), slot, rank, subset)) return;
+    wave_problem<NC>((int)(wid % WaveSet<NC>::count), slot, rank, subset);
     const int mode = kSlotMode[slot];
     const BlockMeta meta = ws.meta[b];
     if (!(meta.valid & (1u << mode)) || (meta.flags & 3u) != 2u) return;
@@ -1241,12 +1242,24 @@ __global__ void __launch_bounds__(256) k_shake_wave(Params p, Workspace ws, cons
     const int nparts = 1 << mi.part_bits;
     const int attempts = nparts < 8 ? nparts : 8;
     if (rank >= attempts) return;
-    const int part = partition_of_rank(ws.qerr + (size_t)b * kQuantTasks + kSlotBase[slot], nparts, rank);
+    // stable rank of every partition, lane = partition (sortProjection order)
+    const int ln = wv::lane();
+    int part;
+    {
+        const double *qe = ws.qerr + (size_t)b * kQuantTasks + kSlotBase[slot];
+        const double v = ln < nparts ? qe[ln] : 0.0;
+        int rk = 0;
+        for (int o = 0; o < nparts; ++o) {
+            const double w = wv::bcast_d(v, o);
+            rk += (w - v < 0 || (!(w - v > 0) && !(w - v < 0) && o < ln)) ? 1 : 0;
+        }
+        const unsigned long long hit = __ballot(ln < nparts && rk == rank);
+        part = hit ? __ffsll((long long)hit) - 1 : 0;
+    }
     const uint64_t qidx = ws.qidx[(size_t)b * kQuantTasks + kSlotBase[slot] + part];
     const ShakeCfg cfg = shake_cfg(mode);
     const float *tex = ws.tex + (size_t)b * 64;
     // gather the subset: lane L < n holds the L-th texel of the subset
-    const int ln = wv::lane();
     uint32_t mask = 0;
     for (int t = 0; t < 16; ++t) mask |= ((int)shape_of(mi.subsets, part, t) == subset ? 1u : 0u) << t;
     const int n = __popc(mask);
@@ -1267,14 +1280,7 @@ __global__ void __launch_bounds__(256) k_shake_wave(Params p, Workspace ws, cons
     int idx = T.live ? (int)((qidx >> (4 * src)) & 15u) : 0;
     int epo[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
     const bool corners_too = !(meta.max_range > 255.0) && cfg.dim == 3;
-    const int nc = cfg.last + 1;
-    double e;
-    if (nc == 4)
-        e = wv::subset_shake<4>(sp, T, idx, epo, corners_too, cfg.shake, cfg.last, cfg.bits, cfg.parity);
-    else if (nc == 8)
-        e = wv::subset_shake<8>(sp, T, idx, epo, corners_too, cfg.shake, cfg.last, cfg.bits, cfg.parity);
-    else
-        e = wv::subset_shake<16>(sp, T, idx, epo, corners_too, cfg.shake, cfg.last, cfg.bits, cfg.parity);
+    const double e = wv::subset_shake<NC>(sp, T, idx, epo, corners_too, cfg.shake, cfg.last, cfg.bits, cfg.parity);
     unsigned long long ti = T.live ? (unsigned long long)(idx & 15) << (4 * src) : 0ull;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) ti |= __shfl_xor(ti, o);
@@ -1647,8 +1653,12 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
         hipLaunchKernelGGL(k_quant, dim3((uint32_t)((nq + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws);
         const uint64_t ns = (uint64_t)p.n * kShakeSlots * kShakeRanks;
         hipLaunchKernelGGL(k_shake, dim3((uint32_t)((ns + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
-        const uint64_t nw = (uint64_t)p.n * kWaveProblems * 64;
-        hipLaunchKernelGGL(k_shake_wave, dim3((uint32_t)((nw + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
+        const uint64_t nw8 = (uint64_t)p.n * WaveSet<8>::count * 64;
+        hipLaunchKernelGGL(k_shake_wave<8>, dim3((uint32_t)((nw8 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
+        const uint64_t nw4 = (uint64_t)p.n * WaveSet<4>::count * 64;
+        hipLaunchKernelGGL(k_shake_wave<4>, dim3((uint32_t)((nw4 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
+        const uint64_t nw16 = (uint64_t)p.n * WaveSet<16>::count * 64;
+        hipLaunchKernelGGL(k_shake_wave<16>, dim3((uint32_t)((nw16 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
         const uint64_t ndq = (uint64_t)p.n * kDualTasks * 2;
         hipLaunchKernelGGL(k_dual_quant, dim3((uint32_t)((ndq + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws);
         const uint64_t nd = (uint64_t)p.n * kDualTasks;
