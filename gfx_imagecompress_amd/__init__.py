@@ -27,7 +27,7 @@ __all__ = [
 
 FMT_BC1, FMT_BC4, FMT_BC5, FMT_BC7 = 1, 4, 5, 7
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libgfx_imagecompress_amd.so")
+LIB_PATH = os.environ.get("GIC_LIBRARY") or os.path.join(_HERE, "lib", "libgfx_imagecompress_amd.so")
 
 GIC_OK, GIC_EINVAL, GIC_EUNSUP, GIC_EHIP = 0, -1, -2, -3
 _ERRS = {GIC_EINVAL: "invalid argument", GIC_EUNSUP: "unsupported option", GIC_EHIP: "HIP runtime error"}

@@ -373,6 +373,8 @@ __device__ double opt_quant(const double data[][4], int n, int ncl, int *index, 
     return err;
 }
 
+#include "bc7_quant.inc"
+
 // -------------------------------------------------------------- shakers ---
 
 __device__ void collapse(int *idx, int n)
@@ -1050,7 +1052,7 @@ __global__ void __launch_bounds__(256) k_quant(Params p, Workspace ws)
     int mode, part;
     task_mode((int)task, mode, part);
     const BlockMeta meta = ws.meta[b];
-    if (!(meta.valid & (1u << mode)) || (meta.flags & 1u)) return;
+    if (!(meta.valid & (1u << mode)) || (meta.flags & 3u)) return;   // integral blocks: k_quant_reg
     const ModeInfo &mi = kModes[mode];
     const int dim = mi.enc == ENC_NO_ALPHA ? 3 : 4;
     const int ncl = 1 << mi.ib0;
@@ -1069,6 +1071,45 @@ __global__ void __launch_bounds__(256) k_quant(Params p, Workspace ws)
         int idx[16];
         err += opt_quant(sub, n, ncl, idx, dim);
         for (int k = 0; k < n; ++k) tidx |= (uint64_t)(idx[k] & 15) << (4 * tex_of[k]);
+    }
+    ws.qerr[(size_t)b * kQuantTasks + task] = err;
+    ws.qidx[(size_t)b * kQuantTasks + task] = tidx;
+}
+
+// K1 (integral blocks): register-resident partition quantisation
+template <int DIM>
+__global__ void __launch_bounds__(256) k_quant_reg(Params p, Workspace ws, int task0, int ntasks)
+{
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t b = gid / ntasks;
+    const int task = task0 + (int)(gid % ntasks);
+    if (b >= p.n) return;
+    int mode, part;
+    task_mode(task, mode, part);
+    const BlockMeta meta = ws.meta[b];
+    if (!(meta.valid & (1u << mode)) || (meta.flags & 3u) != 2u) return;
+    const ModeInfo &mi = kModes[mode];
+    const int ncl = 1 << mi.ib0;
+    const float *tex = ws.tex + (size_t)b * 64;
+    uint32_t px[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const float4 v = *reinterpret_cast<const float4 *>(tex + i * 4);
+        px[i] = (uint32_t)v.x | ((uint32_t)v.y << 8) | ((uint32_t)v.z << 16) | ((uint32_t)v.w << 24);
+    }
+    const uint32_t shape = mi.subsets == 1 ? 0u : (mi.subsets == 2 ? dShape2[part] : dShape3[part]);
+    double err = 0.;
+    uint64_t tidx = 0;
+    for (int sub = 0; sub < mi.subsets; ++sub) {
+        uint32_t mask = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mask |= (((shape >> (2 * i)) & 3u) == (uint32_t)sub ? 1u : 0u) << i;
+        if (!mask) continue;
+        int idx[16];
+        err += opt_quant_mask<DIM>(px, mask, ncl, idx);
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if ((mask >> i) & 1u) tidx |= (uint64_t)(idx[i] & 15) << (4 * i);
     }
     ws.qerr[(size_t)b * kQuantTasks + task] = err;
     ws.qidx[(size_t)b * kQuantTasks + task] = tidx;
@@ -1228,7 +1269,7 @@ __device__ __forceinline__ void wave_problem(int id, int &slot, int &rank, int &
 // K2 (waves): one wavefront per (block, mode, rank, subset) shake problem of
 // an integral block
 template <int NC>
-__global__ void __launch_bounds__(256) k_shake_wave(Params p, Workspace ws, const SpEntry *__restrict__ sp)
+__global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, const SpEntry *__restrict__ sp)
 {
     const uint32_t wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t b = wid / WaveSet<NC>::count;
@@ -1277,6 +1318,7 @@ __global__ void __launch_bounds__(256) k_shake_wave(Params p, Workspace ws, cons
     T.dim = cfg.dim;
     T.live = ln < n;
     for (int j = 0; j < 4; ++j) T.d[j] = (T.live && j < cfg.dim) ? (int)tex[src * 4 + j] : 0;
+    T.d01 = wv::pack16(T.d[0], T.d[1]);
     int idx = T.live ? (int)((qidx >> (4 * src)) & 15u) : 0;
     int epo[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
     const bool corners_too = !(meta.max_range > 255.0) && cfg.dim == 3;
@@ -1297,28 +1339,63 @@ __global__ void __launch_bounds__(256) k_shake_wave(Params p, Workspace ws, cons
 }
 
 // K3a: dual-index quantisation (CompressDualIndexBlock :1084-1152): optQuantAnD_d
-// for the colour and the replicated-alpha halves of each (rotation, selection)
+// for the colour and the replicated-alpha halves of each (rotation, selection);
+// one lane per (block, task, half).  Integral blocks take the register-resident
+// quantiser (k_dual_quant_reg), fractional ones the f64 array path.
+__device__ __forceinline__ void dual_task(uint32_t task, int &mode, int &rot, int &sel)
+{
+    mode = task < 8 ? 4 : 5;
+    rot = task < 8 ? (int)(task >> 1) : (int)(task - 8);
+    sel = task < 8 ? (int)(task & 1) : 0;
+}
+
+__global__ void __launch_bounds__(256) k_dual_quant_reg(Params p, Workspace ws)
+{
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t b = gid / (kDualTasks * 2), r = gid % (kDualTasks * 2);
+    if (b >= p.n) return;
+    const uint32_t task = r >> 1, half = r & 1;
+    int mode, rot, sel;
+    dual_task(task, mode, rot, sel);
+    const BlockMeta meta = ws.meta[b];
+    if (!(meta.valid & (1u << mode)) || (meta.flags & 3u) != 2u) return;
+    const ModeInfo &mi = kModes[mode];
+    const int ncl = 1 << (half ? (sel ? mi.ib0 : mi.ib1) : (sel ? mi.ib1 : mi.ib0));
+    const float *tex = ws.tex + (size_t)b * 64;
+    const int c0 = kRot[rot][half ? 0 : 1], c1 = kRot[rot][half ? 0 : 2], c2 = kRot[rot][half ? 0 : 3];
+    uint32_t px[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        px[i] = (uint32_t)tex[i * 4 + c0] | ((uint32_t)tex[i * 4 + c1] << 8) | ((uint32_t)tex[i * 4 + c2] << 16);
+    int idx[16];
+    opt_quant_mask<3>(px, 0xffffu, ncl, idx);
+    uint64_t ti = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) ti |= (uint64_t)(idx[k] & 15) << (4 * k);
+    ws.dqidx[((size_t)b * kDualTasks + task) * 2 + half] = ti;
+}
+
 __global__ void __launch_bounds__(256) k_dual_quant(Params p, Workspace ws)
 {
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t b = gid / (kDualTasks * 2), r = gid % (kDualTasks * 2);
     if (b >= p.n) return;
     const uint32_t task = r >> 1, half = r & 1;
-    const int mode = task < 8 ? 4 : 5;
-    const int rot = task < 8 ? (int)(task >> 1) : (int)(task - 8);
-    const int sel = task < 8 ? (int)(task & 1) : 0;
+    int mode, rot, sel;
+    dual_task(task, mode, rot, sel);
     const BlockMeta meta = ws.meta[b];
-    if (!(meta.valid & (1u << mode)) || (meta.flags & 1u)) return;
+    if (!(meta.valid & (1u << mode)) || (meta.flags & 3u)) return;
     const ModeInfo &mi = kModes[mode];
     const int ibs[2] = {mi.ib0, mi.ib1};
     const float *tex = ws.tex + (size_t)b * 64;
+    const int ncl = 1 << ibs[half ? 1 ^ sel : sel];
     double blk[16][4];
     for (int i = 0; i < 16; ++i) {
         for (int j = 0; j < 3; ++j) blk[i][j] = (double)tex[i * 4 + kRot[rot][half ? 0 : j + 1]];
         blk[i][3] = 0.0;
     }
     int idx[16];
-    opt_quant(blk, 16, 1 << ibs[half ? 1 ^ sel : sel], idx, 3);
+    opt_quant(blk, 16, ncl, idx, 3);
     uint64_t ti = 0;
     for (int k = 0; k < 16; ++k) ti |= (uint64_t)(idx[k] & 15) << (4 * k);
     ws.dqidx[((size_t)b * kDualTasks + task) * 2 + half] = ti;
@@ -1326,7 +1403,7 @@ __global__ void __launch_bounds__(256) k_dual_quant(Params p, Workspace ws)
 
 // K3b (waves): shakers of one half of a dual-index candidate
 // (CompressDualIndexBlock :1158-1254); integral blocks
-__global__ void __launch_bounds__(256) k_dual_wave(Params p, Workspace ws, const SpEntry *__restrict__ sp)
+__global__ void __launch_bounds__(256, 4) k_dual_wave(Params p, Workspace ws, const SpEntry *__restrict__ sp)
 {
     const uint32_t wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t b = wid / (kDualTasks * 2), r = wid % (kDualTasks * 2);
@@ -1347,6 +1424,7 @@ __global__ void __launch_bounds__(256) k_dual_wave(Params p, Workspace ws, const
     T.live = ln < 16;
     for (int j = 0; j < 3; ++j) T.d[j] = T.live ? (int)tex[ln * 4 + kRot[rot][half ? 0 : j + 1]] : 0;
     T.d[3] = 0;
+    T.d01 = wv::pack16(T.d[0], T.d[1]);
     const uint64_t qi = ws.dqidx[((size_t)b * kDualTasks + task) * 2 + half];
     int idx = T.live ? (int)((qi >> (4 * ln)) & 15u) : 0;
     const int ib = half ? ibs[1 ^ sel] : ibs[sel];
@@ -1651,6 +1729,9 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
             hipLaunchKernelGGL(k_prep_f32, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, blocks, p, st->ws);
         const uint64_t nq = (uint64_t)p.n * kQuantTasks;
         hipLaunchKernelGGL(k_quant, dim3((uint32_t)((nq + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws);
+        const uint64_t nq3 = (uint64_t)p.n * 208, nq4 = (uint64_t)p.n * 65;
+        hipLaunchKernelGGL(k_quant_reg<3>, dim3((uint32_t)((nq3 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, 0, 208);
+        hipLaunchKernelGGL(k_quant_reg<4>, dim3((uint32_t)((nq4 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, 208, 65);
         const uint64_t ns = (uint64_t)p.n * kShakeSlots * kShakeRanks;
         hipLaunchKernelGGL(k_shake, dim3((uint32_t)((ns + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
         const uint64_t nw8 = (uint64_t)p.n * WaveSet<8>::count * 64;
@@ -1661,6 +1742,7 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
         hipLaunchKernelGGL(k_shake_wave<16>, dim3((uint32_t)((nw16 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
         const uint64_t ndq = (uint64_t)p.n * kDualTasks * 2;
         hipLaunchKernelGGL(k_dual_quant, dim3((uint32_t)((ndq + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws);
+        hipLaunchKernelGGL(k_dual_quant_reg, dim3((uint32_t)((ndq + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws);
         const uint64_t nd = (uint64_t)p.n * kDualTasks;
         hipLaunchKernelGGL(k_dual, dim3((uint32_t)((nd + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
         const uint64_t ndw = (uint64_t)p.n * kDualTasks * 2 * 64;

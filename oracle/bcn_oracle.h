@@ -57,6 +57,8 @@ void orc_load_block_rgba8(const uint8_t *src, uint32_t width, uint32_t height,
 uint64_t orc_fnv1a64(const uint8_t *p, size_t n);
 /* BC7 reference-style ramp value used by the shakers (amd_shake.cpp:283-286) */
 int orc_bc7_shake_ramp(int clog, int bits, int p1, int p2, int i);
+/* optQuantAnD_d on caller data, data4 = n x 4 doubles (test hook) */
+double orc_bc7_opt_quant(const double *data4, int n, int ncl, int *index, int dim);
 /* decode one BC7 block to RGBA8 (for tolerance checks) */
 void orc_bc7_decode(const uint8_t blk[16], uint8_t rgba[64]);
 

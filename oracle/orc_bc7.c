@@ -382,6 +382,15 @@ static double opt_quant(double data[][4], int n, int ncl, int *index, double out
     return total_error(data, out, n, dim);
 }
 
+/* test hook: optQuantAnD_d on caller data (n <= 64) */
+double orc_bc7_opt_quant(const double *data4, int n, int ncl, int *index, int dim)
+{
+    double d[64][4], o[64][4];
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < 4; ++j) d[i][j] = data4[i * 4 + j];
+    return opt_quant(d, n, ncl, index, o, dim);
+}
+
 /* -------------------------------------------------------- shakers --- */
 
 /* index_collapse_, amd_shake.cpp:513-538 */
