@@ -51,6 +51,13 @@ static double g_ep[4][256];
 static int g_sp_idx[3][4][256][2][2][16][2];
 static double g_sp_err[3][4][256][2][2][16];
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
+#ifdef ORC_STATS
+/* instrumentation build only (search-shape statistics for kernel design) */
+unsigned long long orc_stats[32];
+#define ST(i, v) __atomic_fetch_add(&orc_stats[i], (unsigned long long)(v), __ATOMIC_RELAXED)
+#else
+#define ST(i, v) ((void)0)
+#endif
 
 static const double kLinW[5][16] = {
     {0.0},
@@ -556,7 +563,7 @@ static void ls_endpoints(double data[][4], const int *cidx, int n, int last, int
 /* ep_shaker_2_d, amd_shake.cpp:703-1053.  index_ updated in place. */
 static double shake_window(double data[][4], int n, int *index_, int epo_code[2][4], int size, int last,
                            int bits, int dim)
-{
+{ ST(5, 1); ST(10, n);
     const int type = bits % (2 * dim);
     const int use_par = (type != 0);
     int mb[4];
@@ -573,6 +580,7 @@ static double shake_window(double data[][4], int n, int *index_, int epo_code[2]
         const int Mi = max_index(index, n);
         int p0 = -1, q0 = -1;
         double err0 = DBL_MAX;
+        ST(6, 1); ST(16 + (Mi < 15 ? Mi : 15), 0);
         if (Mi == 0) {
             double t;
             if (alls) {
@@ -599,7 +607,7 @@ static double shake_window(double data[][4], int n, int *index_, int epo_code[2]
                 double epa[2][4];
                 for (int k = 0; k < n; ++k) cidx[k] = index[k] * q + p;
                 ls_endpoints(data, cidx, n, last, dim, epa);
-                double err1 = DBL_MAX, ed[2][2][4];
+                double err1 = DBL_MAX, ed[2][2][4]; ST(7, 1);
                 int epo1[2][4], best2[2][2][2][4];
                 for (int j = 0; j < dim; ++j) {
                     const int rr = use_par ? 2 : 1;
@@ -615,11 +623,11 @@ static double shake_window(double data[][4], int n, int *index_, int epo_code[2]
                                          (~use_par);
                             }
                             const int step = 1 << use_par;
-                            ed[a][b][j] = DBL_MAX;
+                            ed[a][b][j] = DBL_MAX; ST(8, 1);
                             for (int p1 = lo[0]; p1 <= hi[0]; p1 += step)
                                 for (int p2 = lo[1]; p2 <= hi[1]; p2 += step) {
                                     double t = 0;
-                                    for (int m = n; m > 0; --m) {
+                                    for (int m = n; m > 0; --m) { ST(9, 1);
                                         double rv = shake_ramp(clog, mb[j], p1, p2, cidx[m - 1]);
                                         t += (rv - data[m - 1][j]) * (rv - data[m - 1][j]);
                                     }
@@ -695,7 +703,7 @@ static double shake_window(double data[][4], int n, int *index_, int epo_code[2]
  * epo_code updated in place. */
 static double shake_corners(double data[][4], int n, int *index_, int epo_code[2][4], int last,
                             const int *bits, int type, int dim)
-{
+{ ST(0, 1); ST(11, n);
     const int use_par = (type == PAR_BCC || type == PAR_SAME);
     const int bcc = (type == PAR_BCC);
     const int clog = clog_of(last), nc = 1 << clog;
@@ -708,7 +716,7 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
         collapse(index, n);
         const int Mi = max_index(index, n);
         int p0 = -1, q0 = -1, idx2[16] = {0}, epo2[2][4] = {{0}};
-        double err2 = DBL_MAX;
+        double err2 = DBL_MAX; ST(1, 1); ST(16 + (Mi < 15 ? Mi : 15), 1);
         if (Mi == 0) {
             double t, o2[16][4];
             int epo0[2][4] = {{0}};
@@ -733,12 +741,12 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
         for (int q = 1; q * Mi <= last; ++q)
             for (int p = 0; p <= last - q * Mi; ++p) {
                 int cidx[16], idx1[16] = {0}, epo1[2][4] = {{0}}, s1 = 0;
-                double epa[2][4], err1 = DBL_MAX;
+                double epa[2][4], err1 = DBL_MAX; ST(2, 1);
                 for (int k = 0; k < n; ++k) cidx[k] = index[k] * q + p;
                 ls_endpoints(data, cidx, n, last, dim, epa);
                 for (int odd = 0; odd <= use_par; ++odd)
                     for (int flip = 0; flip <= bcc; ++flip) {
-                        int epi[2][4][2];
+                        int epi[2][4][2]; ST(3, 1); ST(4, n);
                         for (int j = 0; j < dim; ++j)
                             for (int i = 0; i < 2; ++i) {
                                 int f = ep_floor(epa[i][j], bits[j], use_par, (odd ^ (flip & i)) & 1);
