@@ -428,7 +428,7 @@ __device__ __forceinline__ double sp_err(const SpEntry *sp, int c, int b, int v,
 
 // quant_single_point_d, amd_shake.cpp:546-701: best (cluster, endpoint pair)
 // for one point; returns err1 (per point) and the cluster index in idx_out.
-__device__ double single_point_core(const SpEntry *sp, const double point[4], int &idx_out, int epo1[2][4],
+__device__ __noinline__ double single_point_core(const SpEntry *sp, const double point[4], int &idx_out, int epo1[2][4],
                                     int last, const int *bits, int type, int dim)
 {
     double err0 = 1.7976931348623157e308, err1 = 1.7976931348623157e308;
@@ -1313,12 +1313,11 @@ __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, c
                 cnt++;
             }
     }
+    unsigned px = 0;
+    if (ln < n)
+        for (int j = 0; j < cfg.dim; ++j) px |= (unsigned)tex[src * 4 + j] << (8 * j);
     wv::Texels T;
-    T.n = n;
-    T.dim = cfg.dim;
-    T.live = ln < n;
-    for (int j = 0; j < 4; ++j) T.d[j] = (T.live && j < cfg.dim) ? (int)tex[src * 4 + j] : 0;
-    T.d01 = wv::pack16(T.d[0], T.d[1]);
+    wv::make_texels(T, px, n, cfg.dim);
     int idx = T.live ? (int)((qidx >> (4 * src)) & 15u) : 0;
     int epo[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
     const bool corners_too = !(meta.max_range > 255.0) && cfg.dim == 3;
@@ -1418,13 +1417,11 @@ __global__ void __launch_bounds__(256, 4) k_dual_wave(Params p, Workspace ws, co
     const int ibs[2] = {mi.ib0, mi.ib1};
     const float *tex = ws.tex + (size_t)b * 64;
     const int ln = wv::lane();
+    unsigned px = 0;
+    if (ln < 16)
+        for (int j = 0; j < 3; ++j) px |= (unsigned)tex[ln * 4 + kRot[rot][half ? 0 : j + 1]] << (8 * j);
     wv::Texels T;
-    T.n = 16;
-    T.dim = 3;
-    T.live = ln < 16;
-    for (int j = 0; j < 3; ++j) T.d[j] = T.live ? (int)tex[ln * 4 + kRot[rot][half ? 0 : j + 1]] : 0;
-    T.d[3] = 0;
-    T.d01 = wv::pack16(T.d[0], T.d[1]);
+    wv::make_texels(T, px, 16, 3);
     const uint64_t qi = ws.dqidx[((size_t)b * kDualTasks + task) * 2 + half];
     int idx = T.live ? (int)((qi >> (4 * ln)) & 15u) : 0;
     const int ib = half ? ibs[1 ^ sel] : ibs[sel];

@@ -53,10 +53,13 @@ static double g_sp_err[3][4][256][2][2][16];
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
 #ifdef ORC_STATS
 /* instrumentation build only (search-shape statistics for kernel design) */
-unsigned long long orc_stats[32];
-#define ST(i, v) __atomic_fetch_add(&orc_stats[i], (unsigned long long)(v), __ATOMIC_RELAXED)
+unsigned long long orc_stats[9][32];
+static __thread int st_mode = 8;
+#define ST(i, v) __atomic_fetch_add(&orc_stats[st_mode][i], (unsigned long long)(v), __ATOMIC_RELAXED)
+#define ST_MODE(m) (st_mode = (m))
 #else
 #define ST(i, v) ((void)0)
+#define ST_MODE(m) ((void)0)
 #endif
 
 static const double kLinW[5][16] = {
@@ -958,6 +961,7 @@ static void pack_single(const bc7_enc *e, int mode, int part, unsigned colour[3]
 /* CompressSingleIndexBlock, amd_bc7_body.cpp:548-890 */
 static double single_index(bc7_enc *e, double in[16][4], uint8_t out[16], int mode)
 {
+    ST_MODE(mode);
     const mode_info *mi = &kModes[mode];
     const int dim = mi->enc == ENC_NO_ALPHA ? 3 : 4;
     const unsigned nparts = 1u << mi->part_bits;
@@ -1124,6 +1128,7 @@ static void pack_dual(int mode, int sel, int rot, int ep[2][2][4], int idx[2][16
 /* CompressDualIndexBlock, amd_bc7_body.cpp:1059-1278 */
 static double dual_index(bc7_enc *e, double in[16][4], uint8_t out[16], int mode)
 {
+    ST_MODE(mode);
     const mode_info *mi = &kModes[mode];
     const int nrot = 1 << mi->rot_bits, nsel = 1 << mi->idxmode_bits;
     const int ibs[2] = {mi->ib0, mi->ib1};
