@@ -1319,9 +1319,11 @@ __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, c
     wv::Texels T;
     wv::make_texels(T, px, n, cfg.dim);
     int idx = T.live ? (int)((qidx >> (4 * src)) & 15u) : 0;
+    PROF_BEGIN;
     int epo[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
     const bool corners_too = !(meta.max_range > 255.0) && cfg.dim == 3;
     const double e = wv::subset_shake<NC>(sp, T, idx, epo, corners_too, cfg.shake, cfg.last, cfg.bits, cfg.parity);
+    PROF_END;
     unsigned long long ti = T.live ? (unsigned long long)(idx & 15) << (4 * src) : 0ull;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) ti |= __shfl_xor(ti, o);
@@ -1433,10 +1435,10 @@ __global__ void __launch_bounds__(256, 4) k_dual_wave(Params p, Workspace ws, co
     double e;
     if (last == 3) {
         if (corners_too) wv::corners<4>(sp, T, idx, epo, last, bits, PAR_CART);   // Q9: error ignored
-        e = wv::window<4>(sp, T, idx, epo, 6, last, bits[3]);
+        e = wv::window<4, 3>(sp, T, idx, epo, 6, last, bits[3]);
     } else {
         if (corners_too) wv::corners<8>(sp, T, idx, epo, last, bits, PAR_CART);
-        e = wv::window<8>(sp, T, idx, epo, 6, last, bits[3]);
+        e = wv::window<8, 3>(sp, T, idx, epo, 6, last, bits[3]);
     }
     unsigned long long ti = T.live ? (unsigned long long)(idx & 15) << (4 * ln) : 0ull;
 #pragma unroll
@@ -1765,3 +1767,16 @@ hipError_t launch_bc7_blocks(const float *blocks, uint32_t n, const gic_options 
 }
 
 }  // namespace gic
+
+#ifdef GIC_PROFILE
+extern "C" int gic_debug_profile(unsigned long long out[32], int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gic::bc7::wv::g_prof), 32 * sizeof(unsigned long long)) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[32] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(gic::bc7::wv::g_prof), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

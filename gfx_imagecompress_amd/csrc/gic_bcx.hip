@@ -79,36 +79,57 @@ __device__ __forceinline__ void chan_ramp(float r[4], const float ends[2])
         r[e] = floorf((r[0] * (float)(N - 1 - e) + r[N - 1] * (float)e + rnd) / (float)(N - 1));
 }
 
-struct Colours {
-    float c[16][3];   // unique colours, B,G,R, x255
-    float rpt[16];    // repeat counts
+// Unique colours of a block (B,G,R x255 as floats, sorted as QSortFloatCmp)
+// with repeat counts.  Slots i >= n read as colour 0 with count 0, so sums
+// weighted by the count are unchanged by them.  Every loop over colours is a
+// fixed 16-step unrolled loop, which keeps the per-block arrays in VGPRs.
+//   ColB: 8-bit sources -- one word per colour, bytes B, G, R, count.
+//   ColF: float sources (block API).
+//   blk(i, ch) = c(i, ch) / 255.f (FindAxis' input scale); ColB reads it from
+//   the workgroup's byte -> v / 255.0f table (the same value).
+struct ColB {
+    uint32_t u[16];
     int n;
+    const float *lut;   // LDS, 256 entries
+    __device__ __forceinline__ float c(int i, int ch) const { return (float)((u[i] >> (8 * ch)) & 255u); }
+    __device__ __forceinline__ float rpt(int i) const { return (float)(u[i] >> 24); }
+    __device__ __forceinline__ float blk(int i, int ch) const { return lut[(u[i] >> (8 * ch)) & 255u]; }
+};
+struct ColF {
+    float cc[16][3], r[16];
+    int n;
+    __device__ __forceinline__ float c(int i, int ch) const { return cc[i][ch]; }
+    __device__ __forceinline__ float rpt(int i) const { return r[i]; }
+    __device__ __forceinline__ float blk(int i, int ch) const { return cc[i][ch] / 255.f; }
 };
 
 // ClstrErr (weighted), amd_bcx_body.cpp:214-255
-template <int N>
-__device__ float ramp_fit_error(const Colours &u, const float r[3][4], bool flat)
+template <int N, class Col>
+__device__ __forceinline__ float ramp_fit_error(const Col &u, const float r[3][4], bool flat)
 {
     const float w0 = 0.3086f, w1 = 0.6094f, w2 = 0.0820f;
     float err = 0.f;
     const int nr = flat ? 1 : N;
-    for (int i = 0; i < u.n; ++i) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
         float best = 99999999999.f;
-        for (int k = 0; k < nr; ++k) {
-            float d = (u.c[i][CH_R] - r[CH_R][k]) * (u.c[i][CH_R] - r[CH_R][k]) * w0 +
-                      (u.c[i][CH_G] - r[CH_G][k]) * (u.c[i][CH_G] - r[CH_G][k]) * w1 +
-                      (u.c[i][CH_B] - r[CH_B][k]) * (u.c[i][CH_B] - r[CH_B][k]) * w2;
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            if (k >= nr) break;
+            const float cr = u.c(i, CH_R), cg = u.c(i, CH_G), cb = u.c(i, CH_B);
+            float d = (cr - r[CH_R][k]) * (cr - r[CH_R][k]) * w0 + (cg - r[CH_G][k]) * (cg - r[CH_G][k]) * w1 +
+                      (cb - r[CH_B][k]) * (cb - r[CH_B][k]) * w2;
             if (d < best) best = d;
         }
-        err += best * u.rpt[i];
+        err += best * u.rpt(i);   // count 0 past n: adds +0
     }
     return err;
 }
 
 // Refine, amd_bcx_body.cpp:582-806 (R, then G, then B 3x3 jitter of both
 // endpoints on the 565 grid; RefinementSteps = `steps`)
-template <int N>
-__device__ void refine_channels(float cur[3][2], const Colours &u, int steps)
+template <int N, class Col>
+__device__ __forceinline__ void refine_channels(float cur[3][2], const Col &u, int steps)
 {
     const float wr = 0.3086f, wg = 0.6094f, wb = 0.0820f;
     float base[3][2], wk[3][2], r[3][4];
@@ -132,17 +153,18 @@ __device__ void refine_channels(float cur[3][2], const Colours &u, int steps)
 #pragma unroll
             for (int c = 0; c < 3; ++c) chan_ramp<N>(r[c], wk[c]);
         }
-        for (int i = 0; i < u.n; ++i)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
 #pragma unroll
             for (int k = 0; k < N; ++k) {
                 if (ch == CH_R) {
-                    float dg = r[CH_G][k] - u.c[i][CH_G], db = r[CH_B][k] - u.c[i][CH_B];
+                    float dg = r[CH_G][k] - u.c(i, CH_G), db = r[CH_B][k] - u.c(i, CH_B);
                     side[k][i] = dg * dg * wg + db * db * wb;
                 } else if (ch == CH_G) {
-                    float dr = r[CH_R][k] - u.c[i][CH_R], db = r[CH_B][k] - u.c[i][CH_B];
+                    float dr = r[CH_R][k] - u.c(i, CH_R), db = r[CH_B][k] - u.c(i, CH_B);
                     side[k][i] = dr * dr * wr + db * db * wb;
                 } else {
-                    float dr = r[CH_R][k] - u.c[i][CH_R], dg = r[CH_G][k] - u.c[i][CH_G];
+                    float dr = r[CH_R][k] - u.c(i, CH_R), dg = r[CH_G][k] - u.c(i, CH_G);
                     side[k][i] = dr * dr * wr + dg * dg * wg;
                 }
             }
@@ -157,14 +179,17 @@ __device__ void refine_channels(float cur[3][2], const Colours &u, int steps)
                 chan_ramp<N>(r[ch], wk[ch]);
                 float mse = 0.f;
                 const int nr = flat ? 1 : N;
-                for (int i = 0; i < u.n; ++i) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
                     float m = 10000000.f;
-                    for (int k = 0; k < nr; ++k) {
-                        float d = r[ch][k] - u.c[i][ch];
+#pragma unroll
+                    for (int k = 0; k < N; ++k) {
+                        if (k >= nr) break;
+                        float d = r[ch][k] - u.c(i, ch);
                         float e = side[k][i] + d * d * wc;
                         m = minr(m, e);
                     }
-                    mse += m * u.rpt[i];
+                    mse += m * u.rpt(i);   // count 0 past n: adds +0
                 }
                 if (mse < best) {
                     b0 = cur[ch][0];
@@ -177,16 +202,18 @@ __device__ void refine_channels(float cur[3][2], const Colours &u, int steps)
     }
 }
 
-// RampSrchW evaluated in full, amd_bcx_body.cpp:398-435
+// RampSrchW evaluated in full, amd_bcx_body.cpp:398-435.  Entries past n have
+// prem = perr = 0 and prj = 0, so they add +0.
 template <int N>
-__device__ __forceinline__ float proj_ramp_error(const float *prj, const float *perr, const float *prem, float lo,
-                                                 float hi, int n)
+__device__ __forceinline__ float proj_ramp_error(const float prj[16], const float perr[16], const float prem[16],
+                                                 float lo, float hi)
 {
     float error = 0;
     const float step = (hi - lo) / (float)(N - 1);
     const float step_h = step * (float)0.5;
     const float rstep = (float)1.0f / step;
-    for (int i = 0; i < n; ++i) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
         float v, del;
         if ((del = prj[i] - lo) <= 0)
             v = lo;
@@ -201,31 +228,38 @@ __device__ __forceinline__ float proj_ramp_error(const float *prj, const float *
     return error;
 }
 
-// FindAxis, amd_bcx_body.cpp:442-570
-__device__ void principal_axis(float sh[16][3], float dir[3], float centre[3], bool &small, const float blk[16][3],
-                               const float *rpt, int n)
+// FindAxis, amd_bcx_body.cpp:442-570.  The centred colours sh = blk - centre
+// are recomputed where needed (bit-identical each time) instead of stored.
+template <class Col>
+__device__ __forceinline__ void principal_axis(float dir[3], float centre[3], bool &small, const Col &u)
 {
     float crr[3] = {0, 0, 0}, var[3] = {0, 0, 0};
     dir[0] = dir[1] = dir[2] = 0.f;
     centre[0] = centre[1] = centre[2] = 0.f;
     float npts = 0.f;
-    for (int i = 0; i < n; ++i) {
-        centre[0] += blk[i][0] * rpt[i];
-        centre[1] += blk[i][1] * rpt[i];
-        centre[2] += blk[i][2] * rpt[i];
-        npts += rpt[i];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (i < u.n) {
+            centre[0] += u.blk(i, 0) * u.rpt(i);
+            centre[1] += u.blk(i, 1) * u.rpt(i);
+            centre[2] += u.blk(i, 2) * u.rpt(i);
+            npts += u.rpt(i);
+        }
     }
     centre[0] /= npts;
     centre[1] /= npts;
     centre[2] /= npts;
-    for (int i = 0; i < n; ++i) {
-        sh[i][0] = blk[i][0] - centre[0];
-        sh[i][1] = blk[i][1] - centre[1];
-        sh[i][2] = blk[i][2] - centre[2];
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            var[j] += sh[i][j] * sh[i][j] * rpt[i];
-            crr[j] += sh[i][j] * sh[i][(j + 1) % 3] * rpt[i];
+    for (int i = 0; i < 16; ++i) {
+        if (i < u.n) {
+            float sh[3];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) sh[j] = u.blk(i, j) - centre[j];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                var[j] += sh[j] * sh[j] * u.rpt(i);
+                crr[j] += sh[j] * sh[(j + 1) % 3] * u.rpt(i);
+            }
         }
     }
     int i0 = 0, k = 0;
@@ -246,12 +280,15 @@ __device__ void principal_axis(float sh[16][3], float dir[3], float centre[3], b
     small = (var[0] < eps2) && (var[1] < eps2) && (var[2] < eps2);
     if (small) return;
     if (k == 1) {
-        dir[i0] = 1.f;
+        dir[0] = i0 == 0 ? 1.f : 0.f;
+        dir[1] = i0 == 1 ? 1.f : 0.f;
+        dir[2] = i0 == 2 ? 1.f : 0.f;
     } else if (k == 2) {
         const int i1 = (var[(i0 + 1) % 3] > 0.f) ? (i0 + 1) % 3 : (i0 + 2) % 3;
         const float cr = (i1 == (i0 + 1) % 3) ? crr[i0] : crr[(i0 + 2) % 3];
-        dir[i1] = cr / var[i0];
-        dir[i0] = 1.f;
+        const float q = cr / var[i0];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) dir[j] = (j == i1) ? q : (j == i0 ? 1.f : 0.f);
     } else {
         float best_det = 100000.f;
 #pragma unroll
@@ -268,9 +305,8 @@ __device__ void principal_axis(float sh[16][3], float dir[3], float centre[3], b
         float s1 = b * u0 + c * u1;
         s0 /= best_det;
         s1 /= best_det;
-        dir[i0] = 1.f;
-        dir[(i0 + 1) % 3] = 1.f;
-        dir[(i0 + 2) % 3] = s0 + s1;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) dir[j] = (j == (i0 + 2) % 3) ? s0 + s1 : 1.f;
     }
     float len = dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2];
     len = sqrtf(len);
@@ -278,33 +314,38 @@ __device__ void principal_axis(float sh[16][3], float dir[3], float centre[3], b
     for (int j = 0; j < 3; ++j) dir[j] = (len > 0.f) ? dir[j] / len : 0.f;
 }
 
+template <class Col>
+__device__ __forceinline__ float last_colour(const Col &u, int j)
+{
+    float v = u.c(0, j);
+#pragma unroll
+    for (int k = 1; k < 16; ++k) v = (u.n - 1 == k) ? u.c(k, j) : v;
+    return v;
+}
+
 // CompressRGBBlockX, amd_bcx_body.cpp:937-1203
-template <int N>
-__device__ void fit_endpoints(float result[3][2], const Colours &u, int steps)
+template <int N, class Col>
+__device__ __forceinline__ void fit_endpoints(float result[3][2], const Col &u, int steps)
 {
     float rc[3][2];
     bool done = false;
     if (u.n <= 2) {
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            rc[j][0] = u.c[0][j];
-            rc[j][1] = u.c[u.n - 1][j];
+            rc[j][0] = u.c(0, j);
+            rc[j][1] = last_colour(u, j);
         }
         done = true;
     }
-    float sh[16][3], mid[3], dir[3];
+    float mid[3], dir[3];
     if (!done) {
-        float blk[16][3];
-        for (int i = 0; i < u.n; ++i)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) blk[i][j] = u.c[i][j] / 255.f;
         bool small = true;
-        principal_axis(sh, dir, mid, small, blk, u.rpt, u.n);
+        principal_axis(dir, mid, small, u);
         if (small) {
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
-                rc[j][0] = u.c[0][j];
-                rc[j][1] = u.c[u.n - 1][j];
+                rc[j][0] = u.c(0, j);
+                rc[j][1] = last_colour(u, j);
             }
             done = true;
         }
@@ -312,24 +353,33 @@ __device__ void fit_endpoints(float result[3][2], const Colours &u, int steps)
     if (!done) {
         float err_g = 10000000.f;
         float dir_g[3] = {0, 0, 0}, pos_g[2] = {0, 0};
-        float prj0[16], prj[16], perr[16], prem[16];
+        float prj[16], perr[16], prem[16];
         for (;;) {
             float bnd0 = 1000.f, bnd1 = -1000.f;
-            for (int i = 0; i < u.n; ++i) {
-                prj0[i] = prj[i] = sh[i][0] * dir[0] + sh[i][1] * dir[1] + sh[i][2] * dir[2];
-                perr[i] = (sh[i][0] - dir[0] * prj[i]) * (sh[i][0] - dir[0] * prj[i]) +
-                          (sh[i][1] - dir[1] * prj[i]) * (sh[i][1] - dir[1] * prj[i]) +
-                          (sh[i][2] - dir[2] * prj[i]) * (sh[i][2] - dir[2] * prj[i]);
-                bnd0 = minr(bnd0, prj[i]);
-                bnd1 = maxr(bnd1, prj[i]);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                float sh[3];
+#pragma unroll
+                for (int j = 0; j < 3; ++j) sh[j] = u.blk(i, j) - mid[j];
+                const float q = sh[0] * dir[0] + sh[1] * dir[1] + sh[2] * dir[2];
+                const float e = (sh[0] - dir[0] * q) * (sh[0] - dir[0] * q) +
+                                (sh[1] - dir[1] * q) * (sh[1] - dir[1] * q) +
+                                (sh[2] - dir[2] * q) * (sh[2] - dir[2] * q);
+                prj[i] = q;
+                perr[i] = i < u.n ? e : 0.f;
+                if (i < u.n) {
+                    bnd0 = minr(bnd0, q);
+                    bnd1 = maxr(bnd1, q);
+                }
             }
             const float scl0 = bnd0 - (bnd1 - bnd0) * 0.125f;
             const float scl1 = bnd1 + (bnd1 - bnd0) * 0.125f;
             const float scl2 = (scl1 - scl0) * (scl1 - scl0);
             const float over = 1.f / (scl1 - scl0);
-            for (int i = 0; i < u.n; ++i) {
-                prj[i] = (prj[i] - scl0) * over;
-                prem[i] = u.rpt[i] * scl2;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                prj[i] = i < u.n ? (prj[i] - scl0) * over : 0.f;
+                prem[i] = u.rpt(i) * scl2;   // 0 past n
             }
             bnd0 = (bnd0 - scl0) * over;
             bnd1 = (bnd1 - scl0) * over;
@@ -343,7 +393,7 @@ __device__ void fit_endpoints(float result[3][2], const Colours &u, int steps)
             for (int l = 0; l < 8; ++l, lp += stp) {
                 float hp = he;
                 for (int h = 0; h < 8; ++h, hp -= stp) {
-                    const float e = proj_ramp_error<N>(prj, perr, prem, lp, hp, u.n);
+                    const float e = proj_ramp_error<N>(prj, perr, prem, lp, hp);
                     if (e < err) {
                         err = e;
                         pos0 = lp;
@@ -366,19 +416,26 @@ __device__ void fit_endpoints(float result[3][2], const Colours &u, int steps)
             const float over_n = 1.f / (float)(N - 1);
             const float avg = (float)(N - 1) / 2.f;
             float crs[3] = {0, 0, 0}, len = 0.f;
-            for (int i = 0; i < u.n; ++i) {
-                float ri, del;
-                if ((del = prj0[i] - pos0) <= 0)
-                    ri = 0.f;
-                else if (prj0[i] - pos1 >= 0)
-                    ri = (float)(N - 1);
-                else
-                    ri = floorf((del + step_h) * rstep);
-                ri = (ri - avg) * over_n;
-                const float pm = ri * u.rpt[i];
-                len += ri * pm;
 #pragma unroll
-                for (int j = 0; j < 3; ++j) crs[j] += sh[i][j] * pm;
+            for (int i = 0; i < 16; ++i) {
+                if (i < u.n) {
+                    float sh[3];
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) sh[j] = u.blk(i, j) - mid[j];
+                    const float p0 = sh[0] * dir[0] + sh[1] * dir[1] + sh[2] * dir[2];   // prj0[i]
+                    float ri, del;
+                    if ((del = p0 - pos0) <= 0)
+                        ri = 0.f;
+                    else if (p0 - pos1 >= 0)
+                        ri = (float)(N - 1);
+                    else
+                        ri = floorf((del + step_h) * rstep);
+                    ri = (ri - avg) * over_n;
+                    const float pm = ri * u.rpt(i);
+                    len += ri * pm;
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) crs[j] += sh[j] * pm;
+                }
             }
             dir[0] = dir[1] = dir[2] = 0.f;
             if (len > 0.f) {
@@ -401,13 +458,77 @@ __device__ void fit_endpoints(float result[3][2], const Colours &u, int steps)
     refine_channels<N>(result, u, steps);
 }
 
-// Unique colours of the texels kept by the alpha test, sorted by the R,G,B
-// bit patterns (QSortFloatCmp, amd_bcx_body.cpp:103-117) with repeat counts
-// (:1242-1262).  Works by ranking instead of moving records.
-__device__ void unique_colours(Colours &u, const float in[64], bool use_alpha, float thr01, int &kept)
+// Leaders and ranks of the kept texels' colour keys: a kept texel leads its
+// colour group if no earlier kept texel has the same key; its unique index is
+// the number of leaders with a smaller key (QSortFloatCmp order,
+// amd_bcx_body.cpp:103-117, dedupe :1242-1262).
+__device__ __forceinline__ void rank_keys(const uint32_t key[16], bool lead[16], int ui[16], int cnt[16])
+{
+    // key: 24-bit colour key of a kept texel, 0xffffffff for a dropped one
+    // (never equal to or below a kept key)
+    int rank[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        int less = 0, same_before = 0, same = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            same += key[j] == key[i] ? 1 : 0;
+            if (j < i) same_before += key[j] == key[i] ? 1 : 0;
+            less += key[j] < key[i] ? 1 : 0;
+        }
+        lead[i] = key[i] != 0xffffffffu && same_before == 0;
+        cnt[i] = same;
+        rank[i] = lead[i] ? less : 0x7fff;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        int k = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) k += rank[j] < rank[i] ? 1 : 0;
+        ui[i] = k;
+    }
+}
+
+// 8-bit source: px[i] = R | G << 8 | B << 16 | A << 24.  thr_keep is the
+// smallest alpha byte a with a / 255.0f >= alpha threshold (CompRGBABlock's
+// keep test), computed on the host in the same float arithmetic.
+__device__ __forceinline__ void unique_colours(ColB &u, const uint32_t px[16], bool use_alpha, uint32_t thr_keep,
+                                               int &kept)
+{
+    uint32_t key[16];
+    bool lead[16];
+    int ui[16], cnt[16];
+    kept = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const bool live = !use_alpha || (px[i] >> 24) >= thr_keep;
+        // the float keys compare as (R, G, B) bit patterns; for v / 255.0f
+        // values that is the byte order
+        key[i] = live ? ((px[i] & 0xffu) << 16) | (px[i] & 0xff00u) | ((px[i] >> 16) & 0xffu) : 0xffffffffu;
+        kept += live ? 1 : 0;
+    }
+    rank_keys(key, lead, ui, cnt);
+    u.n = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) u.u[k] = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (!lead[i]) continue;
+        // colour as B, G, R bytes + count: (float)byte == (float)((double)(v / 255.0f) * 255.0)
+        const uint32_t w = ((px[i] >> 16) & 0xffu) | (px[i] & 0xff00u) | ((px[i] & 0xffu) << 16) |
+                           ((uint32_t)cnt[i] << 24);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) u.u[k] = (ui[i] == k) ? w : u.u[k];
+        u.n++;
+    }
+}
+
+// float source (block API)
+__device__ __forceinline__ void unique_colours(ColF &u, const float in[64], bool use_alpha, float thr01, int &kept)
 {
     uint32_t key[16][3];
-    bool live[16];
+    bool live[16], lead[16];
+    int rank[16], cnt[16];
     kept = 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -417,9 +538,6 @@ __device__ void unique_colours(Colours &u, const float in[64], bool use_alpha, f
         key[i][2] = __float_as_uint(in[i * 4 + 0]);   // R
         kept += live[i] ? 1 : 0;
     }
-    // a live texel leads its colour group if no earlier live texel has the same key
-    int rank[16], cnt[16];
-    bool lead[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         int less = 0, same_before = 0, same = 0;
@@ -436,27 +554,52 @@ __device__ void unique_colours(Colours &u, const float in[64], bool use_alpha, f
         }
         lead[i] = live[i] && same_before == 0;
         cnt[i] = same;
-        rank[i] = less;   // number of live texels with a smaller key
+        rank[i] = less;
     }
-    // unique index of a leader = number of leaders with a smaller key
     u.n = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        u.cc[k][0] = u.cc[k][1] = u.cc[k][2] = 0.f;
+        u.r[k] = 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         if (!lead[i]) continue;
         int ui = 0;
 #pragma unroll
         for (int j = 0; j < 16; ++j) ui += (lead[j] && (rank[j] < rank[i])) ? 1 : 0;
-        u.c[ui][0] = (float)((double)in[i * 4 + 2] * 255.0);
-        u.c[ui][1] = (float)((double)in[i * 4 + 1] * 255.0);
-        u.c[ui][2] = (float)((double)in[i * 4 + 0] * 255.0);
-        u.rpt[ui] = (float)cnt[i];
+        const float cb = (float)((double)in[i * 4 + 2] * 255.0), cg = (float)((double)in[i * 4 + 1] * 255.0),
+                    cr = (float)((double)in[i * 4 + 0] * 255.0);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (ui == k) {
+                u.cc[k][0] = cb;
+                u.cc[k][1] = cg;
+                u.cc[k][2] = cr;
+                u.r[k] = (float)cnt[i];
+            }
         u.n++;
     }
 }
 
+// Texel access for the final clustering: R, G, B as in * 255.0f and the
+// alpha test !(A * 255 >= thr * 255).
+struct TexB {
+    const uint32_t *px;
+    uint32_t thr_final;   // smallest alpha byte a with (float)a >= thr01 * 255.f
+    __device__ __forceinline__ float ch(int i, int c) const { return (float)((px[i] >> (8 * c)) & 255u); }
+    __device__ __forceinline__ bool transparent(int i) const { return (px[i] >> 24) < thr_final; }
+};
+struct TexF {
+    const float *in;
+    float thr;   // thr01 * 255.f
+    __device__ __forceinline__ float ch(int i, int c) const { return in[i * 4 + c] * 255.0f; }
+    __device__ __forceinline__ bool transparent(int i) const { return !(in[i * 4 + 3] * 255.0f >= thr); }
+};
+
 // Clstr -> ClstrBas -> ClstrIntnl, amd_bcx_body.cpp:258-378
-template <int N>
-__device__ uint32_t final_indices(const float in[64], const uint8_t ep[3][2], bool use_alpha, float thr01, float &err)
+template <int N, class Tex>
+__device__ __forceinline__ uint32_t final_indices(const Tex &t, const uint8_t ep[3][2], bool use_alpha, float &err)
 {
     const float w0 = 0.3086f, w1 = 0.6094f, w2 = 0.0820f;
     const unsigned c0 = ((unsigned)(ep[CH_R][0] & 0xf8) << 8) | ((unsigned)(ep[CH_G][0] & 0xfc) << 3) |
@@ -473,21 +616,21 @@ __device__ uint32_t final_indices(const float in[64], const uint8_t ep[3][2], bo
     const bool flat = expand_grid(wk, ends);
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) chan_ramp<N>(r[ch], wk[ch]);
-    const float thr = thr01 * 255.f;
     const int nr = flat ? 1 : N;
     uint32_t bits = 0;
     err = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        const float R = in[i * 4 + 0] * 255.0f, G = in[i * 4 + 1] * 255.0f, B = in[i * 4 + 2] * 255.0f;
-        const float A = in[i * 4 + 3] * 255.0f;
+        const float R = t.ch(i, 0), G = t.ch(i, 1), B = t.ch(i, 2);
         uint32_t idx;
-        if (use_alpha && !(A >= thr)) {
+        if (use_alpha && t.transparent(i)) {
             idx = N;
         } else {
             float best = 99999999999.f;
             int bi = 0;
-            for (int k = 0; k < nr; ++k) {
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                if (k >= nr) break;
                 const float d = (R - r[CH_R][k]) * (R - r[CH_R][k]) * w0 + (G - r[CH_G][k]) * (G - r[CH_G][k]) * w1 +
                                 (B - r[CH_B][k]) * (B - r[CH_B][k]) * w2;
                 if (d < best) {
@@ -509,9 +652,9 @@ __device__ uint32_t final_indices(const float in[64], const uint8_t ep[3][2], bo
 
 // CompRGBABlock, amd_bcx_body.cpp:1209-1297.  Returns the float error (FLT_MAX
 // for a 4-colour ramp over transparent texels).
-template <int N>
-__device__ float comp_rgba(const float in[64], int steps, bool use_alpha, float thr01, uint8_t ep[3][2],
-                           uint32_t &ibits, const Colours &u, int kept)
+template <int N, class Col, class Tex>
+__device__ __forceinline__ float comp_rgba(const Tex &t, int steps, bool use_alpha, uint8_t ep[3][2], uint32_t &ibits,
+                                           const Col &u, int kept)
 {
     if (!kept) {
 #pragma unroll
@@ -531,24 +674,26 @@ __device__ float comp_rgba(const float in[64], int steps, bool use_alpha, float 
         ep[ch][1] = (uint8_t)res[ch][1];
     }
     float err;
-    ibits = final_indices<N>(in, ep, use_alpha, thr01, err);
+    ibits = final_indices<N>(t, ep, use_alpha, err);
     return err;
 }
 
 // Image_CompressAMDBC1Block, amd_bcx_helpers.cpp:51-105
-__device__ uint2 encode_bc1(const float in[64], int steps, float thr01)
+template <class Col, class Tex>
+__device__ __forceinline__ uint2 encode_bc1(const Col &u, int kept, const Tex &t, int steps, bool use_alpha)
 {
-    const bool use_alpha = thr01 > 0.0f;
-    Colours u;
-    int kept;
-    unique_colours(u, in, use_alpha, thr01, kept);
     uint8_t ep3[3][2], ep4[3][2];
     uint32_t i3 = 0, i4 = 0;
-    const double e3 = comp_rgba<3>(in, steps, use_alpha, thr01, ep3, i3, u, kept);
+    const double e3 = comp_rgba<3>(t, steps, use_alpha, ep3, i3, u, kept);
     double e4 = 3.402823466e+38;
-    if (!(e3 == 0.0)) e4 = comp_rgba<4>(in, steps, use_alpha, thr01, ep4, i4, u, kept);
+    if (!(e3 == 0.0)) e4 = comp_rgba<4>(t, steps, use_alpha, ep4, i4, u, kept);
     const bool m4 = !(e3 <= e4);
-    const uint8_t(*ep)[2] = m4 ? ep4 : ep3;
+    uint8_t ep[3][2];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        ep[ch][0] = m4 ? ep4[ch][0] : ep3[ch][0];
+        ep[ch][1] = m4 ? ep4[ch][1] : ep3[ch][1];
+    }
     const unsigned c0 = ((unsigned)(ep[CH_R][0] >> 3) << 11) | ((unsigned)(ep[CH_G][0] >> 2) << 5) |
                         (unsigned)(ep[CH_B][0] >> 3);
     const unsigned c1 = ((unsigned)(ep[CH_R][1] >> 3) << 11) | ((unsigned)(ep[CH_G][1] >> 2) << 5) |
@@ -560,6 +705,27 @@ __device__ uint2 encode_bc1(const float in[64], int steps, float thr01)
         out.x = c0 | (c1 << 16);
     out.y = m4 ? i4 : i3;
     return out;
+}
+
+__device__ __forceinline__ uint2 encode_bc1_u8(const uint32_t px[16], int steps, bool use_alpha, uint32_t thr_keep,
+                                               uint32_t thr_final, const float *lut)
+{
+    ColB u;
+    u.lut = lut;
+    int kept;
+    unique_colours(u, px, use_alpha, thr_keep, kept);
+    const TexB t{px, thr_final};
+    return encode_bc1(u, kept, t, steps, use_alpha);
+}
+
+__device__ __forceinline__ uint2 encode_bc1_f32(const float in[64], int steps, float thr01)
+{
+    const bool use_alpha = thr01 > 0.0f;
+    ColF u;
+    int kept;
+    unique_colours(u, in, use_alpha, thr01, kept);
+    const TexF t{in, thr01 * 255.f};
+    return encode_bc1(u, kept, t, steps, use_alpha);
 }
 
 // ------------------------------------------------------------- BC4 ---
@@ -781,17 +947,21 @@ struct Bc1Params {
     float alpha_threshold;
     int steps;
     int force_alpha_one;
+    uint32_t thr_keep, thr_final;   // alpha-byte forms of the two threshold tests
 };
 
 __global__ void __launch_bounds__(256) bc1_image_kernel(Geometry g, Bc1Params p, uint2 *__restrict__ dst)
 {
+    __shared__ float lut[256];   // byte -> v / 255.0f
+    lut[threadIdx.x] = (float)threadIdx.x / 255.0f;
+    __syncthreads();
     const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
     if (id >= g.total) return;
     uint32_t slice, by, bx;
     block_coords(g, id, slice, by, bx);
-    float blk[64];
-    load_block(g, slice, by, bx, p.force_alpha_one != 0, blk);
-    dst[id] = bcx::encode_bc1(blk, p.steps, p.alpha_threshold);
+    uint32_t px[16];
+    load_block_u8(g, slice, by, bx, p.force_alpha_one != 0, px);
+    dst[id] = bcx::encode_bc1_u8(px, p.steps, p.alpha_threshold > 0.0f, p.thr_keep, p.thr_final, lut);
 }
 
 __global__ void __launch_bounds__(256) bc45_image_kernel(Geometry g, int fmt, int channel,
@@ -827,7 +997,7 @@ __global__ void __launch_bounds__(256) bc1_blocks_kernel(const float *__restrict
     float blk[64];
 #pragma unroll
     for (int i = 0; i < 64; ++i) blk[i] = blocks[(size_t)id * 64 + i];
-    dst[id] = bcx::encode_bc1(blk, p.steps, p.alpha_threshold);
+    dst[id] = bcx::encode_bc1_f32(blk, p.steps, p.alpha_threshold);
 }
 
 __global__ void __launch_bounds__(256) bc4_blocks_kernel(const float *__restrict__ blocks, uint32_t n,
@@ -843,10 +1013,26 @@ __global__ void __launch_bounds__(256) bc4_blocks_kernel(const float *__restrict
 
 // ------------------------------------------------------------ launchers ---
 
+// smallest alpha byte passing `pass(a)` (256 if none); pass is monotone in a
+template <class F>
+static uint32_t first_byte(F pass)
+{
+    for (uint32_t a = 0; a < 256; ++a)
+        if (pass(a)) return a;
+    return 256;
+}
+
 hipError_t launch_bc1_image(const Geometry &g, float thr, int steps, int force_alpha_one, void *dst,
                             hipStream_t s)
 {
-    const Bc1Params p{thr, steps, force_alpha_one};
+    // CompRGBABlock keeps a texel when a / 255.0f >= thr; ClstrIntnl marks it
+    // transparent when !(a / 255.0f * 255.0f >= thr * 255.f), and a / 255.0f *
+    // 255.0f == a for every byte.  Both tests are monotone in a.
+    const volatile float t = thr;
+    const float t255 = t * 255.f;
+    const uint32_t keep = first_byte([&](uint32_t a) { return (float)a / 255.0f >= t; });
+    const uint32_t fin = first_byte([&](uint32_t a) { return (float)a >= t255; });
+    const Bc1Params p{thr, steps, force_alpha_one, keep, fin};
     const uint32_t wg = 256, grid = (g.total + wg - 1) / wg;
     hipLaunchKernelGGL(bc1_image_kernel, dim3(grid), dim3(wg), 0, s, g, p, (uint2 *)dst);
     return hipGetLastError();
@@ -861,7 +1047,7 @@ hipError_t launch_bc45_image(const Geometry &g, int fmt, int channel, void *dst,
 
 hipError_t launch_bc1_blocks(const float *blocks, uint32_t n, float thr, int steps, void *dst, hipStream_t s)
 {
-    const Bc1Params p{thr, steps, 0};
+    const Bc1Params p{thr, steps, 0, 0u, 0u};
     const uint32_t wg = 256, grid = (n + wg - 1) / wg;
     hipLaunchKernelGGL(bc1_blocks_kernel, dim3(grid), dim3(wg), 0, s, blocks, n, p, (uint2 *)dst);
     return hipGetLastError();

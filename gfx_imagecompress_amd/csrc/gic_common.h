@@ -84,4 +84,45 @@ __device__ __forceinline__ void load_block(const Geometry &g, uint32_t slice, ui
     }
 }
 
+// The same gather as packed RGBA8 words (R | G << 8 | B << 16 | A << 24):
+// missing channels read 0 (alpha 255), the float view of a byte v is v / 255.0f.
+__device__ __forceinline__ void load_block_u8(const Geometry &g, uint32_t slice, uint32_t by, uint32_t bx,
+                                              bool force_alpha_one, uint32_t out[16])
+{
+    const uint8_t *img = g.src + (size_t)slice * g.row_pitch * g.height;
+    const uint32_t x0 = bx * 4, y0 = by * 4;
+    if (g.channels == 4 && x0 + 4 <= g.width && y0 + 4 <= g.height && (g.row_pitch & 15) == 0 &&
+        ((uintptr_t)g.src & 15) == 0) {
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+            const uint4 row = *reinterpret_cast<const uint4 *>(img + (size_t)(y0 + y) * g.row_pitch + x0 * 4);
+            out[y * 4 + 0] = row.x;
+            out[y * 4 + 1] = row.y;
+            out[y * 4 + 2] = row.z;
+            out[y * 4 + 3] = row.w;
+        }
+    } else {
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+            uint32_t sy = y0 + y;
+            sy = sy >= g.height ? g.height - 1 : sy;
+#pragma unroll
+            for (int x = 0; x < 4; ++x) {
+                uint32_t sx = x0 + x;
+                sx = sx >= g.width ? g.width - 1 : sx;
+                const uint8_t *p = img + (size_t)sy * g.row_pitch + (size_t)sx * g.channels;
+                uint32_t w = p[0];
+                if (g.channels > 1) w |= (uint32_t)p[1] << 8;
+                if (g.channels > 2) w |= (uint32_t)p[2] << 16;
+                w |= (g.channels > 3 ? (uint32_t)p[3] : 255u) << 24;
+                out[y * 4 + x] = w;
+            }
+        }
+    }
+    if (force_alpha_one || g.channels < 4) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) out[i] |= 0xff000000u;
+    }
+}
+
 }  // namespace gic

@@ -759,6 +759,32 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
                                                      : (1 << use_par)) &
                                                 (~use_par);
                             }
+#ifdef ORC_STATS
+                        { /* pass lower bound: per texel, channels choose options independently */
+                            double lb = 0;
+                            for (int i = 0; i < n; ++i) {
+                                double best = DBL_MAX;
+                                for (int c = 0; c < nc; ++c) {
+                                    double t = 0;
+                                    for (int j = 0; j < dim; ++j) {
+                                        double bj = DBL_MAX;
+                                        for (int o = 0; o < 4; ++o) {
+                                            double rv = shake_ramp(clog, bits[j], epi[0][j][o & 1], epi[1][j][o >> 1], c);
+                                            double dv = (rv - data[i][j]) * (rv - data[i][j]);
+                                            bj = dv < bj ? dv : bj;
+                                        }
+                                        t += bj;
+                                    }
+                                    best = t < best ? t : best;
+                                }
+                                lb += best;
+                            }
+                            const double thr = err1 < err2 ? err1 : err2;
+                            ST(12, 1);
+                            if (lb >= thr) ST(13, 1);
+                            if (lb >= err1) ST(14, 1);
+                        }
+#endif
                         /* 64-corner Gray-code walk :1273-1341; evaluated per corner */
                         int s = 0;
                         for (int p1 = 0; p1 < 64; ++p1) {
