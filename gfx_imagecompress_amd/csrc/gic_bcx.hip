@@ -87,12 +87,26 @@ __device__ __forceinline__ void chan_ramp(float r[4], const float ends[2])
 //   ColF: float sources (block API).
 //   blk(i, ch) = c(i, ch) / 255.f (FindAxis' input scale); ColB reads it from
 //   the workgroup's byte -> v / 255.0f table (the same value).
+// Byte -> float conversions as opaque single instructions: the compiler would
+// otherwise hoist all 48 of them out of the search loops and run out of VGPRs.
+__device__ __forceinline__ float ubyte_f(uint32_t w, int b)
+{
+    float r;
+    switch (b) {
+    case 0: asm volatile("v_cvt_f32_ubyte0 %0, %1" : "=v"(r) : "v"(w)); break;
+    case 1: asm volatile("v_cvt_f32_ubyte1 %0, %1" : "=v"(r) : "v"(w)); break;
+    case 2: asm volatile("v_cvt_f32_ubyte2 %0, %1" : "=v"(r) : "v"(w)); break;
+    default: asm volatile("v_cvt_f32_ubyte3 %0, %1" : "=v"(r) : "v"(w)); break;
+    }
+    return r;
+}
+
 struct ColB {
     uint32_t u[16];
     int n;
-    const float *lut;   // LDS, 256 entries
-    __device__ __forceinline__ float c(int i, int ch) const { return (float)((u[i] >> (8 * ch)) & 255u); }
-    __device__ __forceinline__ float rpt(int i) const { return (float)(u[i] >> 24); }
+    const volatile float *lut;   // LDS, 256 entries (volatile: re-read, not hoisted)
+    __device__ __forceinline__ float c(int i, int ch) const { return ubyte_f(u[i], ch); }
+    __device__ __forceinline__ float rpt(int i) const { return ubyte_f(u[i], 3); }
     __device__ __forceinline__ float blk(int i, int ch) const { return lut[(u[i] >> (8 * ch)) & 255u]; }
 };
 struct ColF {
@@ -708,7 +722,7 @@ __device__ __forceinline__ uint2 encode_bc1(const Col &u, int kept, const Tex &t
 }
 
 __device__ __forceinline__ uint2 encode_bc1_u8(const uint32_t px[16], int steps, bool use_alpha, uint32_t thr_keep,
-                                               uint32_t thr_final, const float *lut)
+                                               uint32_t thr_final, const volatile float *lut)
 {
     ColB u;
     u.lut = lut;
@@ -950,7 +964,7 @@ struct Bc1Params {
     uint32_t thr_keep, thr_final;   // alpha-byte forms of the two threshold tests
 };
 
-__global__ void __launch_bounds__(256) bc1_image_kernel(Geometry g, Bc1Params p, uint2 *__restrict__ dst)
+__global__ void __launch_bounds__(256, 2) bc1_image_kernel(Geometry g, Bc1Params p, uint2 *__restrict__ dst)
 {
     __shared__ float lut[256];   // byte -> v / 255.0f
     lut[threadIdx.x] = (float)threadIdx.x / 255.0f;
