@@ -1078,7 +1078,7 @@ __global__ void __launch_bounds__(256) k_quant(Params p, Workspace ws)
 
 // K1 (integral blocks): register-resident partition quantisation
 template <int DIM>
-__global__ void __launch_bounds__(256) k_quant_reg(Params p, Workspace ws, int task0, int ntasks)
+__global__ void __launch_bounds__(256, 2) k_quant_reg(Params p, Workspace ws, int task0, int ntasks)
 {
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t b = gid / ntasks;
@@ -1350,7 +1350,7 @@ __device__ __forceinline__ void dual_task(uint32_t task, int &mode, int &rot, in
     sel = task < 8 ? (int)(task & 1) : 0;
 }
 
-__global__ void __launch_bounds__(256) k_dual_quant_reg(Params p, Workspace ws)
+__global__ void __launch_bounds__(256, 2) k_dual_quant_reg(Params p, Workspace ws)
 {
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t b = gid / (kDualTasks * 2), r = gid % (kDualTasks * 2);
