@@ -47,6 +47,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--traffic-json", default="")
+    p.add_argument("--bc7-rows", type=int, default=-1,
+                   help="with the default BC1 workload, also time BC7 on this many block rows of the same "
+                        "texture (-1 = the whole 8K texture, 0 = skip)")
     return p.parse_args()
 
 
@@ -93,6 +96,60 @@ def cpu_baseline(fmt, src_host, size, gpu_blocks, budget_s, avail_rows):
                      f"{dt:.1f} s, {threads} threads)",
            "blocks_per_s": round(rows * bx / dt, 1)}
     return res, parity, mism
+
+
+def bc7_secondary(args, gic, src, size, avail_rows, world, dev, rank):
+    """BC7 default quality (configs[3]) on the same texture: one timed pass over
+    `--bc7-rows` block rows per rank after a short warm-up, plus (rank 0) the
+    CPU restatement on one block row with a bit-exactness check."""
+    import torch
+    import torch.distributed as dist
+    bx = (size + 3) // 4
+    rows = avail_rows if args.bc7_rows < 0 else min(args.bc7_rows, avail_rows)
+    dst = torch.empty(bx * rows * 16, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    gic.encode_device(7, src, size, size, 1, 4, dst, gic.Options(), 0, min(rows, 4), stream=stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    gic.encode_device(7, src, size, size, 1, 4, dst, gic.Options(), 0, rows, stream=stream)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    t = torch.tensor([wall, ev0.elapsed_time(ev1)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall, kern_ms = float(t[0]), float(t[1])
+    px = size * rows * 4 * world
+    res = {"metric": "Mpixels/s BC7 default quality (quality 1, all modes, shakers on)",
+           "value": round(px / wall / 1e6, 4), "unit": "Mpixels/s",
+           "blocks_per_s": round(bx * rows * world / wall, 1), "ms_per_pass": round(wall * 1e3, 2),
+           "kernel_ms": round(kern_ms, 2), "rows_per_gpu": rows * 4, "dtype": "f64+int32",
+           "roofline": {"bound": "valu", "alg_bytes_per_launch": 80 * bx * rows,
+                        "hbm_frac": round(80 * bx * rows / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 8)}}
+    if rank == 0 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+        threads = max(1, min(threads, os.cpu_count() or 1, 64))
+        host = src.cpu().numpy()[0]
+        c0 = time.perf_counter()
+        ref = oracle_lib.encode_image(7, host, first_row=0, num_rows=1, threads=threads)
+        dt = time.perf_counter() - c0
+        got = dst.cpu().numpy().reshape(-1, 16)[:bx]
+        same = int((got == ref).all(axis=1).sum())
+        res["cpu_baseline"] = {"value": round(4 * size / dt / 1e6, 5), "unit": "Mpixels/s", "cores": threads,
+                               "kind": "port", "sample": f"block row 0 ({bx} blocks, {dt:.1f} s, {threads} threads)",
+                               "blocks_per_s": round(bx / dt, 1)}
+        res["gpu_parity"] = f"{same}/{bx} blocks of the sampled row bit-identical"
+    return res
 
 
 def main():
@@ -171,6 +228,10 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
+    bc7 = None
+    if fmt == 1 and args.bc7_rows != 0:
+        bc7 = bc7_secondary(args, gic, src, size, rows, world, dev, rank)
+
     cpu = None
     parity = None
     if rank == 0 and not args.no_cpu:
@@ -208,6 +269,8 @@ def main():
         }
         if gather_ms is not None:
             line["gather_ms"] = round(gather_ms, 3)
+        if bc7 is not None:
+            line["bc7"] = bc7
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
