@@ -228,13 +228,11 @@ __device__ __forceinline__ float proj_ramp_error(const float prj[16], const floa
     const float rstep = (float)1.0f / step;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        float v, del;
-        if ((del = prj[i] - lo) <= 0)
-            v = lo;
-        else if (prj[i] - hi >= 0)
-            v = hi;
-        else
-            v = floorf((del + step_h) * rstep) * step + lo;
+        // branch-free form of: del <= 0 ? lo : prj - hi >= 0 ? hi : snapped
+        const float del = prj[i] - lo;
+        const float q = floorf((del + step_h) * rstep) * step + lo;
+        const float vh = (prj[i] - hi >= 0) ? hi : q;
+        const float v = (del <= 0) ? lo : vh;
         float d = prj[i] - v;
         d *= d;
         error += prem[i] * d + perr[i];
