@@ -129,11 +129,10 @@ __device__ __forceinline__ float ramp_fit_error(const Col &u, const float r[3][4
         float best = 99999999999.f;
 #pragma unroll
         for (int k = 0; k < N; ++k) {
-            if (k >= nr) break;
             const float cr = u.c(i, CH_R), cg = u.c(i, CH_G), cb = u.c(i, CH_B);
             float d = (cr - r[CH_R][k]) * (cr - r[CH_R][k]) * w0 + (cg - r[CH_G][k]) * (cg - r[CH_G][k]) * w1 +
                       (cb - r[CH_B][k]) * (cb - r[CH_B][k]) * w2;
-            if (d < best) best = d;
+            best = (k < nr && d < best) ? d : best;
         }
         err += best * u.rpt(i);   // count 0 past n: adds +0
     }
@@ -198,10 +197,9 @@ __device__ __forceinline__ void refine_channels(float cur[3][2], const Col &u, i
                     float m = 10000000.f;
 #pragma unroll
                     for (int k = 0; k < N; ++k) {
-                        if (k >= nr) break;
                         float d = r[ch][k] - u.c(i, ch);
                         float e = side[k][i] + d * d * wc;
-                        m = minr(m, e);
+                        m = (k < nr) ? minr(m, e) : m;
                     }
                     mse += m * u.rpt(i);   // count 0 past n: adds +0
                 }
