@@ -428,7 +428,7 @@ __device__ __forceinline__ double sp_err(const SpEntry *sp, int c, int b, int v,
 
 // quant_single_point_d, amd_shake.cpp:546-701: best (cluster, endpoint pair)
 // for one point; returns err1 (per point) and the cluster index in idx_out.
-__device__ __noinline__ double single_point_core(const SpEntry *sp, const double point[4], int &idx_out, int epo1[2][4],
+__device__ double single_point_core(const SpEntry *sp, const double point[4], int &idx_out, int epo1[2][4],
                                     int last, const int *bits, int type, int dim)
 {
     double err0 = 1.7976931348623157e308, err1 = 1.7976931348623157e308;
