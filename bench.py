@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--traffic-json", default="")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="nccl (= RCCL, the real multi-GPU path) or gloo (rehearsal with ranks sharing a GPU)")
     p.add_argument("--bc7-rows", type=int, default=-1,
                    help="with the default BC1 workload, also time BC7 on this many block rows of the same "
                         "texture (-1 = the whole 8K texture, 0 = skip)")
@@ -98,6 +100,33 @@ def cpu_baseline(fmt, src_host, size, gpu_blocks, budget_s, avail_rows):
     return res, parity, mism
 
 
+def _max_over_ranks(t, world):
+    """All-reduce MAX of a small float64 tensor (RCCL on the device, or on the
+    host for the gloo rehearsal)."""
+    import torch.distributed as dist
+    if world <= 1:
+        return t
+    if dist.get_backend() == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.MAX)
+        return h
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t
+
+
+def _gather_all(dst, world):
+    """All-gather of every rank's packed blocks into one buffer."""
+    import torch
+    import torch.distributed as dist
+    if dist.get_backend() == "gloo":
+        parts = [torch.empty_like(dst, device="cpu") for _ in range(world)]
+        dist.all_gather(parts, dst.cpu())
+        return torch.cat(parts)
+    out_all = torch.empty(world * dst.numel(), dtype=torch.uint8, device=dst.device)
+    dist.all_gather_into_tensor(out_all, dst)
+    return out_all
+
+
 def bc7_secondary(args, gic, src, size, avail_rows, world, dev, rank):
     """BC7 default quality (configs[3]) on the same texture: one timed pass over
     `--bc7-rows` block rows per rank after a short warm-up, plus (rank 0) the
@@ -123,9 +152,7 @@ def bc7_secondary(args, gic, src, size, avail_rows, world, dev, rank):
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    t = torch.tensor([wall, ev0.elapsed_time(ev1)], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = _max_over_ranks(torch.tensor([wall, ev0.elapsed_time(ev1)], dtype=torch.float64, device=dev), world)
     wall, kern_ms = float(t[0]), float(t[1])
     px = size * rows * 4 * world
     res = {"metric": "Mpixels/s BC7 default quality (quality 1, all modes, shakers on)",
@@ -161,10 +188,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dist_backend == "gloo":
+        # rehearsal of the N>1 logic with more ranks than GPUs (ranks share devices)
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     fmt = FMTS[args.format]
     size = args.size
@@ -198,20 +231,19 @@ def main():
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps
-    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = _max_over_ranks(torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev), world)
     wall, kern_ms = float(t[0]), float(t[1])
 
     gather_ms = None
     if args.gather and world > 1:
-        out_all = torch.empty(world * dst.numel(), dtype=torch.uint8, device=dev)
         torch.cuda.synchronize(dev)
         dist.barrier()
         g0 = time.perf_counter()
-        dist.all_gather_into_tensor(out_all, dst)
+        out_all = _gather_all(dst, world)
         torch.cuda.synchronize(dev)
         gather_ms = (time.perf_counter() - g0) * 1e3
+        if out_all.numel() != world * dst.numel():
+            raise RuntimeError("gather returned a wrong size")
 
     pixels = size * rows * 4 * world          # pixels encoded per step, all ranks
     value = pixels * args.steps / wall / 1e6

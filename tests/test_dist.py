@@ -51,6 +51,41 @@ def _image(fmt, ch):
     return np.ascontiguousarray(np.stack(sl)), w, h, s
 
 
+def _bench_worker(rank, world, port, q):
+    try:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        t = bench._max_over_ranks(torch.tensor([1.0 + rank, 10.0 - rank], dtype=torch.float64), world)
+        g = bench._gather_all(torch.full((5,), rank + 1, dtype=torch.uint8), world)
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, (t.tolist(), g.tolist())))
+    except Exception as e:   # pragma: no cover
+        q.put((rank, repr(e)))
+
+
+def test_bench_reductions_two_ranks():
+    """bench.py's max-over-ranks timing reduction and bitstream gather (gloo path)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert not isinstance(got[r], str), got[r]
+        t, g = got[r]
+        assert t == [2.0, 10.0]
+        assert g == [1] * 5 + [2] * 5
+
+
 def _worker(rank, world, port, q):
     try:
         import sys
