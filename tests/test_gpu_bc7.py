@@ -121,3 +121,15 @@ def test_bc7_8k_sampled_rows(gpu):
         ref = oracle_lib.encode_image(7, img, first_row=row, num_rows=1)[:256]
         check_tolerance(out, ref, _src_blocks(img, row, 1)[:256])
         assert np.array_equal(out, ref), _mismatch_report(out, ref)
+
+
+def test_bc7_4096_seeded_random_blocks(gpu):
+    """SURVEY.md 8(d) random-block sample: 4096 seeded blocks of uniform RGBA
+    noise (half of them opaque), every block against the oracle."""
+    rng = np.random.default_rng(20261015)
+    img = rng.integers(0, 256, (256, 256, 4), dtype=np.uint8)
+    img[:128, :, 3] = 255
+    out = gpu_encode(7, img)
+    ref = oracle_lib.encode_image(7, img)
+    check_tolerance(out, ref, _src_blocks(img))
+    assert np.array_equal(out, ref), _mismatch_report(out, ref)
