@@ -214,23 +214,37 @@ __device__ __forceinline__ void refine_channels(float cur[3][2], const Col &u, i
     }
 }
 
-// RampSrchW evaluated in full, amd_bcx_body.cpp:398-435.  Entries past n have
-// prem = perr = 0 and prj = 0, so they add +0.
+// RampSrchW, amd_bcx_body.cpp:398-435, over entries [I0, I1) continuing the
+// running sum `error`.  Entries past n have prem = perr = 0 and prj = 0, so
+// they add +0.  (prj - hi >= 0 is prj >= hi and del <= 0 is prj <= lo for
+// IEEE floats with denormals kept.)
+struct RampStep {
+    float lo, hi, step, step_h, rstep;
+};
+
 template <int N>
-__device__ __forceinline__ float proj_ramp_error(const float prj[16], const float perr[16], const float prem[16],
-                                                 float lo, float hi)
+__device__ __forceinline__ RampStep ramp_step(float lo, float hi)
 {
-    float error = 0;
-    const float step = (hi - lo) / (float)(N - 1);
-    const float step_h = step * (float)0.5;
-    const float rstep = (float)1.0f / step;
+    RampStep r;
+    r.lo = lo;
+    r.hi = hi;
+    r.step = (hi - lo) / (float)(N - 1);
+    r.step_h = r.step * (float)0.5;
+    r.rstep = (float)1.0f / r.step;
+    return r;
+}
+
+template <int I0, int I1>
+__device__ __forceinline__ float proj_ramp_error(float error, const float prj[16], const float perr[16],
+                                                 const float prem[16], const RampStep &r)
+{
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = I0; i < I1; ++i) {
         // branch-free form of: del <= 0 ? lo : prj - hi >= 0 ? hi : snapped
-        const float del = prj[i] - lo;
-        const float q = floorf((del + step_h) * rstep) * step + lo;
-        const float vh = (prj[i] - hi >= 0) ? hi : q;
-        const float v = (del <= 0) ? lo : vh;
+        const float del = prj[i] - r.lo;
+        const float q = floorf((del + r.step_h) * r.rstep) * r.step + r.lo;
+        const float vh = (prj[i] >= r.hi) ? r.hi : q;
+        const float v = (prj[i] <= r.lo) ? r.lo : vh;
         float d = prj[i] - v;
         d *= d;
         error += prem[i] * d + perr[i];
@@ -403,7 +417,12 @@ __device__ __forceinline__ void fit_endpoints(float result[3][2], const Col &u, 
             for (int l = 0; l < 8; ++l, lp += stp) {
                 float hp = he;
                 for (int h = 0; h < 8; ++h, hp -= stp) {
-                    const float e = proj_ramp_error<N>(prj, perr, prem, lp, hp);
+                    // the terms are non-negative: once every block of the wave
+                    // has reached its best error after 8 entries, the rest
+                    // cannot make this candidate win (RampSrchW's own early out)
+                    const RampStep rs = ramp_step<N>(lp, hp);
+                    float e = proj_ramp_error<0, 8>(0.f, prj, perr, prem, rs);
+                    if (!__all(e >= err)) e = proj_ramp_error<8, 16>(e, prj, perr, prem, rs);
                     if (e < err) {
                         err = e;
                         pos0 = lp;
