@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--traffic-json", default="")
+    p.add_argument("--bc7-quality", type=float, default=1.0,
+                   help="BC7BlockEncoder quality for BC7 runs (reference image API: 1.0)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL, the real multi-GPU path) or gloo (rehearsal with ranks sharing a GPU)")
     p.add_argument("--bc7-rows", type=int, default=-1,
@@ -67,7 +69,7 @@ def make_source(fmt, size, rank, device):
     return torch.from_numpy(synth.normal_map(h)[None].copy()).to(device)
 
 
-def cpu_baseline(fmt, src_host, size, gpu_blocks, budget_s, avail_rows):
+def cpu_baseline(fmt, src_host, size, gpu_blocks, budget_s, avail_rows, bc7_quality=1.0):
     """Oracle on a bounded prefix of block rows; returns (dict, parity_ok)."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -77,8 +79,13 @@ def cpu_baseline(fmt, src_host, size, gpu_blocks, budget_s, avail_rows):
     bx = (size + 3) // 4
     by = min((size + 3) // 4, avail_rows)
     rows = min(by, 2 if fmt == 7 else 16)
+
+    def run(n):
+        if fmt == 7:
+            return oracle_lib.encode_image_bc7(src_host, quality=bc7_quality, first_row=0, num_rows=n, threads=threads)
+        return oracle_lib.encode_image(fmt, src_host, bc4_channel=0, first_row=0, num_rows=n, threads=threads)
     t0 = time.perf_counter()
-    out = oracle_lib.encode_image(fmt, src_host, bc4_channel=0, first_row=0, num_rows=rows, threads=threads)
+    out = run(rows)
     dt = time.perf_counter() - t0
     # grow the sample to ~budget_s of CPU work (bounded by the image)
     if dt < budget_s / 4 and rows < by:
@@ -87,7 +94,7 @@ def cpu_baseline(fmt, src_host, size, gpu_blocks, budget_s, avail_rows):
         if more > rows:
             rows = more
             t0 = time.perf_counter()
-            out = oracle_lib.encode_image(fmt, src_host, bc4_channel=0, first_row=0, num_rows=rows, threads=threads)
+            out = run(rows)
             dt = time.perf_counter() - t0
     px = rows * 4 * size
     gpu_rows = gpu_blocks.reshape(-1, bx, out.shape[1])[:rows].reshape(out.shape)
@@ -137,7 +144,8 @@ def bc7_secondary(args, gic, src, size, avail_rows, world, dev, rank):
     rows = avail_rows if args.bc7_rows < 0 else min(args.bc7_rows, avail_rows)
     dst = torch.empty(bx * rows * 16, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
-    gic.encode_device(7, src, size, size, 1, 4, dst, gic.Options(), 0, min(rows, 4), stream=stream)
+    opts = gic.Options(bc7_quality=args.bc7_quality)
+    gic.encode_device(7, src, size, size, 1, 4, dst, opts, 0, min(rows, 4), stream=stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -145,7 +153,7 @@ def bc7_secondary(args, gic, src, size, avail_rows, world, dev, rank):
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    gic.encode_device(7, src, size, size, 1, 4, dst, gic.Options(), 0, rows, stream=stream)
+    gic.encode_device(7, src, size, size, 1, 4, dst, opts, 0, rows, stream=stream)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -155,7 +163,7 @@ def bc7_secondary(args, gic, src, size, avail_rows, world, dev, rank):
     t = _max_over_ranks(torch.tensor([wall, ev0.elapsed_time(ev1)], dtype=torch.float64, device=dev), world)
     wall, kern_ms = float(t[0]), float(t[1])
     px = size * rows * 4 * world
-    res = {"metric": "Mpixels/s BC7 default quality (quality 1, all modes, shakers on)",
+    res = {"metric": f"Mpixels/s BC7 quality {args.bc7_quality:g} (all modes, shakers on)",
            "value": round(px / wall / 1e6, 4), "unit": "Mpixels/s",
            "blocks_per_s": round(bx * rows * world / wall, 1), "ms_per_pass": round(wall * 1e3, 2),
            "kernel_ms": round(kern_ms, 2), "rows_per_gpu": rows * 4, "dtype": "f64+int32",
@@ -168,7 +176,7 @@ def bc7_secondary(args, gic, src, size, avail_rows, world, dev, rank):
         threads = max(1, min(threads, os.cpu_count() or 1, 64))
         host = src.cpu().numpy()[0]
         c0 = time.perf_counter()
-        ref = oracle_lib.encode_image(7, host, first_row=0, num_rows=1, threads=threads)
+        ref = oracle_lib.encode_image_bc7(host, quality=args.bc7_quality, first_row=0, num_rows=1, threads=threads)
         dt = time.perf_counter() - c0
         got = dst.cpu().numpy().reshape(-1, 16)[:bx]
         same = int((got == ref).all(axis=1).sum())
@@ -207,7 +215,7 @@ def main():
     ch = CHANNELS[fmt]
     nblocks = bx * rows
     dst = torch.empty(nblocks * gic.block_bytes(fmt), dtype=torch.uint8, device=dev)
-    opts = gic.Options(bc4_channel=0)
+    opts = gic.Options(bc4_channel=0, bc7_quality=args.bc7_quality)
     stream = torch.cuda.current_stream(dev)
 
     def step():
@@ -269,7 +277,7 @@ def main():
     if rank == 0 and not args.no_cpu:
         host = src.cpu().numpy()[0]
         torch.cuda.synchronize(dev)
-        cpu, parity, mism = cpu_baseline(fmt, host, size, dst.cpu().numpy(), args.cpu_seconds, rows)
+        cpu, parity, mism = cpu_baseline(fmt, host, size, dst.cpu().numpy(), args.cpu_seconds, rows, args.bc7_quality)
         cpu["gpu_parity"] = "bit-exact" if parity else f"{mism} blocks differ"
 
     if rank == 0:

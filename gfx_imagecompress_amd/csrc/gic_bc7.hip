@@ -98,6 +98,7 @@ struct Workspace {
     ShakeResult *shk;      // [n][6][8]
     DualResult *dual;      // [n][12]
     uint64_t *dqidx;       // [n][12][2] optQuantAnD_d indices of the dual-index candidates
+    double *dqerr;         // [n][12][2] their optQuantAnD_d errors (quality <= 0.7 gating)
 };
 
 __device__ __forceinline__ int expand_code(int bits, int v) { return (v << (8 - bits)) | (v >> (2 * bits - 8)); }
@@ -968,7 +969,32 @@ struct Params {
     int colour_restrict, alpha_restrict, force_alpha_one;
     uint32_t n;        // blocks in this chunk
     uint32_t first;    // first block id of the chunk within the launch
+    // BC7BlockEncoder's quality-derived settings (amd_bc7_body.hpp:94-149),
+    // computed on the host exactly as the constructor does
+    double quality, shake_thr, err_thr, part_search;
 };
+
+// partitions quantised (CompressSingleIndexBlock :569-573) and shaken (:695-706)
+__device__ __forceinline__ int mode_tries(const Params &p, int mode)
+{
+    const unsigned nparts = 1u << kModes[mode].part_bits;
+    unsigned tries = nparts;
+    if (p.quality < 0.5) {
+        tries = (unsigned)floor((double)(tries * p.part_search) + 0.5);
+        tries = tries < 1 ? 1 : tries;
+        tries = tries > nparts ? nparts : tries;
+    }
+    return (int)tries;
+}
+
+__device__ __forceinline__ int mode_attempts(const Params &p, int mode)
+{
+    const unsigned tries = (unsigned)mode_tries(p, mode);
+    unsigned attempts = (unsigned)floor(8 * p.quality + 0.5);
+    attempts = attempts < tries ? attempts : tries;
+    attempts = attempts > 1 ? attempts : 1;
+    return (int)attempts;
+}
 
 __device__ void prep_block(const float inN[64], const Params &p, float *tex, BlockMeta &meta)
 {
@@ -1053,6 +1079,7 @@ __global__ void __launch_bounds__(256) k_quant(Params p, Workspace ws)
     task_mode((int)task, mode, part);
     const BlockMeta meta = ws.meta[b];
     if (!(meta.valid & (1u << mode)) || (meta.flags & 3u)) return;   // integral blocks: k_quant_reg
+    if (part >= mode_tries(p, mode)) return;
     const ModeInfo &mi = kModes[mode];
     const int dim = mi.enc == ENC_NO_ALPHA ? 3 : 4;
     const int ncl = 1 << mi.ib0;
@@ -1088,6 +1115,7 @@ __global__ void __launch_bounds__(256, 2) k_quant_reg(Params p, Workspace ws, in
     task_mode(task, mode, part);
     const BlockMeta meta = ws.meta[b];
     if (!(meta.valid & (1u << mode)) || (meta.flags & 3u) != 2u) return;
+    if (part >= mode_tries(p, mode)) return;
     const ModeInfo &mi = kModes[mode];
     const int ncl = 1 << mi.ib0;
     const float *tex = ws.tex + (size_t)b * 64;
@@ -1137,12 +1165,12 @@ __device__ double shake_subset(const SpEntry *sp, const double sub[][4], const T
     return e1;
 }
 
-// Shake parameters of a single-index mode (amd_bc7_body.cpp:654-706, quality 1)
+// Shake parameters of a single-index mode (amd_bc7_body.cpp:654-706)
 struct ShakeCfg {
     int dim, parity, last, shake, bits[4];
 };
 
-__device__ ShakeCfg shake_cfg(int mode)
+__device__ ShakeCfg shake_cfg(int mode, double quality)
 {
     const ModeInfo &mi = kModes[mode];
     ShakeCfg c;
@@ -1165,9 +1193,10 @@ __device__ ShakeCfg shake_cfg(int mode)
         c.bits[3] += 2;
     else if (c.parity == PAR_SAME)
         c.bits[3] += 1;
-    int shake = 8 - (int)floor(1.5 * mi.ib0);
-    shake = shake < 6 ? shake : 6;   // quality 1: floor(shake * 1 + 0.5) = shake
-    shake = shake > 2 ? shake : 2;
+    const unsigned s0 = 8 - (unsigned)floor(1.5 * mi.ib0);
+    unsigned t = (unsigned)floor(s0 * quality + 0.5);
+    t = t < 6 ? t : 6;
+    int shake = (int)(t > 2 ? t : 2);
     if (c.parity == PAR_SAME || c.parity == PAR_BCC) shake += 2;
     c.shake = shake;
     c.last = (1 << mi.ib0) - 1;
@@ -1202,16 +1231,15 @@ __global__ void __launch_bounds__(256) k_shake(Params p, Workspace ws, const SpE
     const BlockMeta meta = ws.meta[b];
     if (!(meta.valid & (1u << mode)) || (meta.flags & 3u)) return;   // integral blocks: k_shake_wave
     const ModeInfo &mi = kModes[mode];
-    const int nparts = 1 << mi.part_bits;
-    const int attempts = nparts < 8 ? nparts : 8;
-    if (rank >= attempts) return;
+    const int nparts = mode_tries(p, mode);   // partitions quantised and ranked
+    if (rank >= mode_attempts(p, mode)) return;
     const int part = partition_of_rank(ws.qerr + (size_t)b * kQuantTasks + kSlotBase[slot], nparts, rank);
     const uint64_t qidx = ws.qidx[(size_t)b * kQuantTasks + kSlotBase[slot] + part];
-    const ShakeCfg cfg = shake_cfg(mode);
+    const ShakeCfg cfg = shake_cfg(mode, p.quality);
     const float *tex = ws.tex + (size_t)b * 64;
     ShakeResult &res = ws.shk[((size_t)b * kShakeSlots + slot) * kShakeRanks + rank];
     res.part = (uint32_t)part;
-    const bool corners_too = !(meta.max_range > 255.0) && cfg.dim == 3;   // m_shakerRangeThreshold = 255
+    const bool corners_too = !(meta.max_range > p.shake_thr) && cfg.dim == 3;   // m_shakerRangeThreshold
     for (int s = 0; s < mi.subsets; ++s) {
         double sub[16][4];
         int tex_of[16], n = 0, idx[16];
@@ -1280,9 +1308,8 @@ __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, c
     const BlockMeta meta = ws.meta[b];
     if (!(meta.valid & (1u << mode)) || (meta.flags & 3u) != 2u) return;
     const ModeInfo &mi = kModes[mode];
-    const int nparts = 1 << mi.part_bits;
-    const int attempts = nparts < 8 ? nparts : 8;
-    if (rank >= attempts) return;
+    const int nparts = mode_tries(p, mode);   // partitions quantised and ranked
+    if (rank >= mode_attempts(p, mode)) return;
     // stable rank of every partition, lane = partition (sortProjection order)
     const int ln = wv::lane();
     int part;
@@ -1298,7 +1325,7 @@ __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, c
         part = hit ? __ffsll((long long)hit) - 1 : 0;
     }
     const uint64_t qidx = ws.qidx[(size_t)b * kQuantTasks + kSlotBase[slot] + part];
-    const ShakeCfg cfg = shake_cfg(mode);
+    const ShakeCfg cfg = shake_cfg(mode, p.quality);
     const float *tex = ws.tex + (size_t)b * 64;
     // gather the subset: lane L < n holds the L-th texel of the subset
     uint32_t mask = 0;
@@ -1321,7 +1348,7 @@ __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, c
     int idx = T.live ? (int)((qidx >> (4 * src)) & 15u) : 0;
     PROF_BEGIN;
     int epo[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-    const bool corners_too = !(meta.max_range > 255.0) && cfg.dim == 3;
+    const bool corners_too = !(meta.max_range > p.shake_thr) && cfg.dim == 3;
     const double e = wv::subset_shake<NC>(sp, T, idx, epo, corners_too, cfg.shake, cfg.last, cfg.bits, cfg.parity);
     PROF_END;
     unsigned long long ti = T.live ? (unsigned long long)(idx & 15) << (4 * src) : 0ull;
@@ -1343,6 +1370,32 @@ __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, c
 // for the colour and the replicated-alpha halves of each (rotation, selection);
 // one lane per (block, task, half).  Integral blocks take the register-resident
 // quantiser (k_dual_quant_reg), fractional ones the f64 array path.
+// CompressDualIndexBlock shakes a (rotation, selection) candidate when
+// quality > 0.7 or its quantiser error qe = e_colour + e_alpha / 3 is <= the
+// smallest qe of the mode's earlier candidates (:1141, :1170)
+__device__ __forceinline__ bool dual_shaken(const Params &p, const Workspace &ws, uint32_t b, int task)
+{
+    if (p.quality > 0.7) return true;
+    const int t0 = task < 8 ? 0 : 8;
+    const double *q = ws.dqerr + (size_t)b * kDualTasks * 2;
+    double best_q = 1.7976931348623157e308;
+    for (int t = t0; t < task; ++t) {
+        double qe = q[2 * t];
+        qe += q[2 * t + 1] / 3.;
+        if (qe < best_q) best_q = qe;
+    }
+    double qe = q[2 * task];
+    qe += q[2 * task + 1] / 3.;
+    return qe <= best_q;
+}
+
+__device__ __forceinline__ int dual_shake_size(const Params &p)
+{
+    unsigned shake = (unsigned)(6 * p.quality);
+    shake = shake < 6 ? shake : 6;
+    return (int)(shake > 2 ? shake : 2);
+}
+
 __device__ __forceinline__ void dual_task(uint32_t task, int &mode, int &rot, int &sel)
 {
     mode = task < 8 ? 4 : 5;
@@ -1369,11 +1422,12 @@ __global__ void __launch_bounds__(256, 2) k_dual_quant_reg(Params p, Workspace w
     for (int i = 0; i < 16; ++i)
         px[i] = (uint32_t)tex[i * 4 + c0] | ((uint32_t)tex[i * 4 + c1] << 8) | ((uint32_t)tex[i * 4 + c2] << 16);
     int idx[16];
-    opt_quant_mask<3>(px, 0xffffu, ncl, idx);
+    const double qe = opt_quant_mask<3>(px, 0xffffu, ncl, idx);
     uint64_t ti = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) ti |= (uint64_t)(idx[k] & 15) << (4 * k);
     ws.dqidx[((size_t)b * kDualTasks + task) * 2 + half] = ti;
+    ws.dqerr[((size_t)b * kDualTasks + task) * 2 + half] = qe;
 }
 
 __global__ void __launch_bounds__(256) k_dual_quant(Params p, Workspace ws)
@@ -1396,10 +1450,11 @@ __global__ void __launch_bounds__(256) k_dual_quant(Params p, Workspace ws)
         blk[i][3] = 0.0;
     }
     int idx[16];
-    opt_quant(blk, 16, ncl, idx, 3);
+    const double qe = opt_quant(blk, 16, ncl, idx, 3);
     uint64_t ti = 0;
     for (int k = 0; k < 16; ++k) ti |= (uint64_t)(idx[k] & 15) << (4 * k);
     ws.dqidx[((size_t)b * kDualTasks + task) * 2 + half] = ti;
+    ws.dqerr[((size_t)b * kDualTasks + task) * 2 + half] = qe;
 }
 
 // K3b (waves): shakers of one half of a dual-index candidate
@@ -1415,10 +1470,15 @@ __global__ void __launch_bounds__(256, 4) k_dual_wave(Params p, Workspace ws, co
     const int sel = task < 8 ? (int)(task & 1) : 0;
     const BlockMeta meta = ws.meta[b];
     if (!(meta.valid & (1u << mode)) || (meta.flags & 3u) != 2u) return;
+    const int ln = wv::lane();
+    if (!dual_shaken(p, ws, b, (int)task)) {   // not shaken: never selected
+        if (ln == 0) ws.dual[(size_t)b * kDualTasks + task].err[half] = 1.7976931348623157e308;
+        return;
+    }
+    const int shake = dual_shake_size(p);
     const ModeInfo &mi = kModes[mode];
     const int ibs[2] = {mi.ib0, mi.ib1};
     const float *tex = ws.tex + (size_t)b * 64;
-    const int ln = wv::lane();
     unsigned px = 0;
     if (ln < 16)
         for (int j = 0; j < 3; ++j) px |= (unsigned)tex[ln * 4 + kRot[rot][half ? 0 : j + 1]] << (8 * j);
@@ -1431,14 +1491,14 @@ __global__ void __launch_bounds__(256, 4) k_dual_wave(Params p, Workspace ws, co
     const int cb = half ? mi.scalar_bits : mi.vector_bits / 3;
     const int bits[4] = {cb, cb, cb, half ? 6 * cb : 2 * 3 * cb};
     int epo[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-    const bool corners_too = !(meta.max_range > 255.0);
+    const bool corners_too = !(meta.max_range > p.shake_thr);
     double e;
     if (last == 3) {
         if (corners_too) wv::corners<4>(sp, T, idx, epo, last, bits, PAR_CART);   // Q9: error ignored
-        e = wv::window<4, 3>(sp, T, idx, epo, 6, last, bits[3]);
+        e = wv::window<4, 3>(sp, T, idx, epo, shake, last, bits[3]);
     } else {
         if (corners_too) wv::corners<8>(sp, T, idx, epo, last, bits, PAR_CART);
-        e = wv::window<8, 3>(sp, T, idx, epo, 6, last, bits[3]);
+        e = wv::window<8, 3>(sp, T, idx, epo, shake, last, bits[3]);
     }
     unsigned long long ti = T.live ? (unsigned long long)(idx & 15) << (4 * ln) : 0ull;
 #pragma unroll
@@ -1465,6 +1525,11 @@ __global__ void __launch_bounds__(256) k_dual(Params p, Workspace ws, const SpEn
     const int sel = task < 8 ? (int)(task & 1) : 0;
     const BlockMeta meta = ws.meta[b];
     if (!(meta.valid & (1u << mode)) || (meta.flags & 3u)) return;
+    if (!dual_shaken(p, ws, b, (int)task)) {   // not shaken: never selected
+        ws.dual[(size_t)b * kDualTasks + task].err[0] = 1.7976931348623157e308;
+        ws.dual[(size_t)b * kDualTasks + task].err[1] = 1.7976931348623157e308;
+        return;
+    }
     const ModeInfo &mi = kModes[mode];
     const int ibs[2] = {mi.ib0, mi.ib1};
     const float *tex = ws.tex + (size_t)b * 64;
@@ -1481,13 +1546,13 @@ __global__ void __launch_bounds__(256) k_dual(Params p, Workspace ws, const SpEn
         const uint64_t qi = ws.dqidx[((size_t)b * kDualTasks + task) * 2 + h];
         for (int k = 0; k < 16; ++k) idx[h][k] = (int)((qi >> (4 * k)) & 15u);
     }
-    const int shake = 6;   // max(2, min((uint32_t)(6 * 1.0), 6))
+    const int shake = dual_shake_size(p);
     const int cbits = mi.vector_bits / 3, abits = mi.scalar_bits;
     const int bits0[4] = {cbits, cbits, cbits, 2 * 3 * cbits};
     const int bits1[4] = {abits, abits, abits, 6 * abits};
     const int last0 = (1 << ibs[sel]) - 1, last1 = (1 << ibs[1 ^ sel]) - 1;
     int epo[2][2][4] = {{{0, 0, 0, 0}, {0, 0, 0, 0}}, {{0, 0, 0, 0}, {0, 0, 0, 0}}};
-    const bool corners_too = !(meta.max_range > 255.0);
+    const bool corners_too = !(meta.max_range > p.shake_thr);
     if (corners_too) shake_corners<double>(sp, cb, &cb[0][0], 16, idx[0], epo[0], last0, bits0, PAR_CART);   // Q9
     const double ec = shake_window<double>(sp, cb, &cb[0][0], 16, idx[0], epo[0], shake, last0, bits0[3], 3);
     if (corners_too) shake_corners<double>(sp, ab, &ab[0][0], 16, idx[1], epo[1], last1, bits1, PAR_CART);
@@ -1532,6 +1597,7 @@ __global__ void __launch_bounds__(256) k_select(Params p, Workspace ws, uint4 *_
             double be = 1.7976931348623157e308;
             for (int t = 0; t < nt; ++t) {
                 const DualResult &dr = ws.dual[(size_t)b * kDualTasks + t0 + t];
+                if (dr.err[0] == 1.7976931348623157e308) continue;   // candidate not shaken
                 double v = 0;
                 v += dr.err[0];
                 v += dr.err[1] / 3.;
@@ -1556,8 +1622,7 @@ __global__ void __launch_bounds__(256) k_select(Params p, Workspace ws, uint4 *_
             pack_dual(m, sel, rot, ep, idx, w);
         } else {
             const int slot = m <= 3 ? m : (m == 6 ? 4 : 5);
-            const int nparts = 1 << kModes[m].part_bits;
-            const int attempts = nparts < 8 ? nparts : 8;
+            const int attempts = mode_attempts(p, m);
             const int ns = kModes[m].subsets;
             int bi = 0;
             double be = 1.7976931348623157e308;
@@ -1569,6 +1634,7 @@ __global__ void __launch_bounds__(256) k_select(Params p, Workspace ws, uint4 *_
                     be = v;
                     bi = r;
                 }
+                if (p.err_thr > 0 && be <= p.err_thr) break;   // :837-843
             }
             e = be;
             const ShakeResult &sr = ws.shk[((size_t)b * kShakeSlots + slot) * kShakeRanks + bi];
@@ -1579,6 +1645,7 @@ __global__ void __launch_bounds__(256) k_select(Params p, Workspace ws, uint4 *_
             best = e;
             for (int q = 0; q < 4; ++q) bw[q] = w[q];
         }
+        if (p.err_thr > 0 && best <= p.err_thr) break;   // CompressBlock :1440-1446
     }
     dst[out_id] = make_uint4(bw[0], bw[1], bw[2], bw[3]);
     if (err_out) err_out[out_id] = best;
@@ -1681,7 +1748,8 @@ static hipError_t get_state(uint32_t chunk, DeviceState *&out)
         const size_t sz = align_up(n * 64 * sizeof(float)) + align_up(n * sizeof(BlockMeta)) +
                           align_up(n * kQuantTasks * sizeof(double)) + align_up(n * kQuantTasks * sizeof(uint64_t)) +
                           align_up(n * kShakeSlots * kShakeRanks * sizeof(ShakeResult)) +
-                          align_up(n * kDualTasks * sizeof(DualResult)) + align_up(n * kDualTasks * 2 * sizeof(uint64_t));
+                          align_up(n * kDualTasks * sizeof(DualResult)) + align_up(n * kDualTasks * 2 * sizeof(uint64_t)) +
+                          align_up(n * kDualTasks * 2 * sizeof(double));
         e = hipMalloc(&st.ws_mem, sz);
         if (e != hipSuccess) return e;
         char *p = (char *)st.ws_mem;
@@ -1698,6 +1766,8 @@ static hipError_t get_state(uint32_t chunk, DeviceState *&out)
         st.ws.dual = (DualResult *)p;
         p += align_up(n * kDualTasks * sizeof(DualResult));
         st.ws.dqidx = (uint64_t *)p;
+        p += align_up(n * kDualTasks * 2 * sizeof(uint64_t));
+        st.ws.dqerr = (double *)p;
         st.ws_blocks = chunk;
     }
     out = &st;
@@ -1721,6 +1791,22 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
         p.force_alpha_one = o.force_alpha_one;
         p.first = first;
         p.n = (total - first) < chunk ? (total - first) : chunk;
+        // BC7BlockEncoder constructor (amd_bc7_body.hpp:94-149)
+        const double q = o.bc7_quality;
+        p.quality = q < 1.0 ? (q > 0.0 ? q : 0.0) : 1.0;
+        if (p.quality < 0.5) {
+            p.shake_thr = 0.;
+            p.err_thr = 256. * (1.0 - ((p.quality * 2.0) / 0.5));
+            p.part_search = (1.0 / 16.0) > ((p.quality * 2.0) / 0.5) ? (1.0 / 16.0) : ((p.quality * 2.0) / 0.5);
+        } else if (p.quality < 0.7) {
+            p.shake_thr = 255 * (p.quality / 10);
+            p.err_thr = 256. * (1.0 - (p.quality / 0.5));
+            p.part_search = (1.0 / 16.0) > (p.quality / 0.5) ? (1.0 / 16.0) : (p.quality / 0.5);
+        } else {
+            p.shake_thr = 255 * p.quality;
+            p.err_thr = 0;
+            p.part_search = 1.0;
+        }
         const uint32_t wg = 256;
         if (g)
             hipLaunchKernelGGL(k_prep_image, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, *g, p, st->ws);

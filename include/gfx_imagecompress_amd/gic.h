@@ -48,7 +48,7 @@ typedef struct gic_options {
     uint8_t colour_restrict;     /* default 1 */
     uint8_t alpha_restrict;      /* default 1 */
     uint8_t force_alpha_one;     /* 1: ignore source alpha (ReadNxNBlockF forceAlphaTo1) */
-    float bc7_quality;           /* must be 1.0 in this release */
+    float bc7_quality;           /* BC7BlockEncoder quality, clamped to [0,1] (default 1.0) */
     float bc7_performance;       /* must be 1.0 in this release */
 } gic_options;
 

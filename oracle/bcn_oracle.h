@@ -50,6 +50,13 @@ int orc_encode_image(int fmt, const uint8_t *src, uint32_t width, uint32_t heigh
                      int32_t first_row, int32_t num_rows, int threads,
                      uint8_t *dst, double *block_err);
 
+/* The BC7 block loop with the encoder's quality and ModeMask exposed (the
+ * reference's image API fixes quality 1.0, amd_bc7_compressor.cpp:58-65; the
+ * block API Image_CompressAMDMultiModeLDRBlock takes both). */
+int orc_encode_image_bc7(const uint8_t *src, uint32_t width, uint32_t height, uint32_t slices, uint32_t channels,
+                         int32_t first_row, int32_t num_rows, int threads, float quality, uint8_t mode_mask,
+                         uint8_t *dst, double *block_err);
+
 /* helpers exposed for unit tests */
 void orc_load_block_rgba8(const uint8_t *src, uint32_t width, uint32_t height,
                           uint32_t channels, uint32_t bx, uint32_t by,

@@ -56,6 +56,8 @@ typedef struct {
     uint32_t row0, nrows, bx_count, by_count;
     uint8_t *dst;
     double *err;
+    float bc7_quality;   /* BC7BlockEncoder quality (image API: 1.0) */
+    uint8_t bc7_mask;    /* BC7 ModeMask (image API default 0xFF) */
     int next;            /* next job (slice*nrows + row) */
     int njobs;
     pthread_mutex_t lock;
@@ -93,7 +95,7 @@ static void encode_row(job_t *j, uint32_t slice, uint32_t brow)
             break;
         case 7:
             /* Image_CompressAMDBC7 (amd_bc7_compressor.cpp:58-65) */
-            e = orc_bc7_block(blk, 0xFF, has_alpha, 1.0f, 1, 1, 1.0f, o);
+            e = orc_bc7_block(blk, j->bc7_mask, has_alpha, j->bc7_quality, 1, 1, 1.0f, o);
             break;
         }
         if (j->err) j->err[out_row + bx] = e;
@@ -113,9 +115,9 @@ static void *worker(void *arg)
     return NULL;
 }
 
-int orc_encode_image(int fmt, const uint8_t *src, uint32_t width, uint32_t height, uint32_t slices,
-                     uint32_t channels, int bc4_channel, int32_t first_row, int32_t num_rows,
-                     int threads, uint8_t *dst, double *block_err)
+static int encode_image(int fmt, const uint8_t *src, uint32_t width, uint32_t height, uint32_t slices,
+                        uint32_t channels, int bc4_channel, int32_t first_row, int32_t num_rows, int threads,
+                        float bc7_quality, uint8_t bc7_mask, uint8_t *dst, double *block_err)
 {
     if (!src || !dst || !width || !height || !slices || channels < 1 || channels > 4) return -1;
     if (fmt != 1 && fmt != 4 && fmt != 5 && fmt != 7) return -1;
@@ -128,6 +130,8 @@ int orc_encode_image(int fmt, const uint8_t *src, uint32_t width, uint32_t heigh
     j.slices = slices;
     j.channels = channels;
     j.bc4_channel = bc4_channel;
+    j.bc7_quality = bc7_quality;
+    j.bc7_mask = bc7_mask;
     j.bx_count = (width + 3) / 4;
     j.by_count = (height + 3) / 4;
     j.row0 = first_row < 0 ? 0 : (uint32_t)first_row;
@@ -147,4 +151,20 @@ int orc_encode_image(int fmt, const uint8_t *src, uint32_t width, uint32_t heigh
     }
     pthread_mutex_destroy(&j.lock);
     return 0;
+}
+
+int orc_encode_image(int fmt, const uint8_t *src, uint32_t width, uint32_t height, uint32_t slices,
+                     uint32_t channels, int bc4_channel, int32_t first_row, int32_t num_rows,
+                     int threads, uint8_t *dst, double *block_err)
+{
+    return encode_image(fmt, src, width, height, slices, channels, bc4_channel, first_row, num_rows, threads, 1.0f,
+                        0xFF, dst, block_err);
+}
+
+int orc_encode_image_bc7(const uint8_t *src, uint32_t width, uint32_t height, uint32_t slices, uint32_t channels,
+                         int32_t first_row, int32_t num_rows, int threads, float quality, uint8_t mode_mask,
+                         uint8_t *dst, double *block_err)
+{
+    return encode_image(7, src, width, height, slices, channels, 0, first_row, num_rows, threads, quality,
+                        mode_mask, dst, block_err);
 }

@@ -33,6 +33,10 @@ def lib() -> ctypes.CDLL:
                                           ctypes.c_uint32, ctypes.c_int, ctypes.c_int32, ctypes.c_int32,
                                           ctypes.c_int, vp, vp]
         _lib.orc_encode_image.restype = ctypes.c_int
+        _lib.orc_encode_image_bc7.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                              ctypes.c_int32, ctypes.c_int32, ctypes.c_int, ctypes.c_float,
+                                              ctypes.c_uint8, vp, vp]
+        _lib.orc_encode_image_bc7.restype = ctypes.c_int
         _lib.orc_bc1_block.argtypes = [vp, ctypes.c_int, ctypes.c_float, vp]
         _lib.orc_bc4_block.argtypes = [vp, vp]
         _lib.orc_bc7_block.argtypes = [vp, ctypes.c_uint8, ctypes.c_int, ctypes.c_float, ctypes.c_int,
@@ -66,6 +70,27 @@ def encode_image(fmt: int, img: np.ndarray, bc4_channel: int = 1, first_row: int
     threads = threads or min(os.cpu_count() or 1, 16)
     rc = lib().orc_encode_image(fmt, a.ctypes.data, w, h, s, c, bc4_channel, first_row, num_rows, threads,
                                 out.ctypes.data, err.ctypes.data if want_err else None)
+    if rc != 0:
+        raise RuntimeError(f"oracle encode failed ({rc})")
+    return (out, err) if want_err else out
+
+
+def encode_image_bc7(img: np.ndarray, quality: float = 1.0, mode_mask: int = 0xFF, first_row: int = -1,
+                     num_rows: int = -1, threads: int = 0, want_err: bool = False):
+    """BC7 over an image with the encoder quality / ModeMask of the block API."""
+    a = np.ascontiguousarray(img, dtype=np.uint8)
+    if a.ndim == 2:
+        a = a[:, :, None]
+    if a.ndim == 3:
+        a = a[None]
+    s, h, w, c = a.shape
+    bx, by = (w + 3) // 4, (h + 3) // 4
+    rows = by - max(first_row, 0) if num_rows < 0 else num_rows
+    out = np.zeros((s * rows * bx, 16), np.uint8)
+    err = np.zeros(s * rows * bx, np.float64) if want_err else None
+    threads = threads or min(os.cpu_count() or 1, 16)
+    rc = lib().orc_encode_image_bc7(a.ctypes.data, w, h, s, c, first_row, num_rows, threads, quality, mode_mask,
+                                    out.ctypes.data, err.ctypes.data if want_err else None)
     if rc != 0:
         raise RuntimeError(f"oracle encode failed ({rc})")
     return (out, err) if want_err else out

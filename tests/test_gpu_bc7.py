@@ -133,3 +133,24 @@ def test_bc7_4096_seeded_random_blocks(gpu):
     ref = oracle_lib.encode_image(7, img)
     check_tolerance(out, ref, _src_blocks(img))
     assert np.array_equal(out, ref), _mismatch_report(out, ref)
+
+
+@pytest.mark.parametrize("quality", [0.0, 0.05, 0.2, 0.45, 0.55, 0.65, 0.75, 0.9])
+def test_bc7_quality_levels(gpu, quality):
+    """BC7BlockEncoder quality < 1 (block API Image_CompressAMDMultiModeLDRBlock):
+    fewer partitions, smaller shake windows, corner search by range, error-
+    threshold early exits over partition ranks and modes, quantiser-error
+    gating of dual-index candidates (amd_bc7_body.hpp:94-149)."""
+    g1 = synth.g1(64, 16)
+    noise = synth.noise_rgba(32, 16, seed=7, alpha=True)
+    for img in (g1, noise):
+        import torch
+        src = torch.from_numpy(np.ascontiguousarray(img)[None]).cuda()
+        h, w = img.shape[:2]
+        nb = ((w + 3) // 4) * ((h + 3) // 4)
+        dst = torch.zeros(nb * 16, dtype=torch.uint8, device="cuda")
+        gic.encode_device(7, src, w, h, 1, 4, dst, gic.Options(bc7_quality=quality))
+        torch.cuda.synchronize()
+        out = dst.cpu().numpy().reshape(-1, 16)
+        ref = oracle_lib.encode_image_bc7(img, quality=quality)
+        assert np.array_equal(out, ref), (quality, _mismatch_report(out, ref))
