@@ -72,7 +72,8 @@ __device__ __forceinline__ int sp_index(int clog, int bits, int v, int o1, int o
 
 struct BlockMeta {
     uint32_t valid;        // legal-mode mask after CompressBlock's filtering
-    uint32_t flags;        // bit0: unsupported (needs optQuantTrace_d)
+    uint32_t flags;        // bit0: unsupported (needs optQuantTrace_d), bit1: integral texels,
+                           // bit2: error threshold met (staged low-quality pipeline)
     double max_range;
 };
 
@@ -99,6 +100,8 @@ struct Workspace {
     DualResult *dual;      // [n][12]
     uint64_t *dqidx;       // [n][12][2] optQuantAnD_d indices of the dual-index candidates
     double *dqerr;         // [n][12][2] their optQuantAnD_d errors (quality <= 0.7 gating)
+    double *best_err;      // [n] running best over the modes of earlier stages
+    uint4 *best_blk;       // [n] its packed block
 };
 
 __device__ __forceinline__ int expand_code(int bits, int v) { return (v << (8 - bits)) | (v >> (2 * bits - 8)); }
@@ -972,7 +975,15 @@ struct Params {
     // BC7BlockEncoder's quality-derived settings (amd_bc7_body.hpp:94-149),
     // computed on the host exactly as the constructor does
     double quality, shake_thr, err_thr, part_search;
+    uint32_t stage_mask;   // modes evaluated by this launch sequence (all, or one per stage)
 };
+
+// BlockMeta.flags bit 2: the block met the error threshold in an earlier
+// stage (CompressBlock's mode-loop exit, :1440-1446)
+__device__ __forceinline__ bool mode_active(const BlockMeta &meta, const Params &p, int mode)
+{
+    return (meta.valid & p.stage_mask & (1u << mode)) && !(meta.flags & 4u);
+}
 
 // partitions quantised (CompressSingleIndexBlock :569-573) and shaken (:695-706)
 __device__ __forceinline__ int mode_tries(const Params &p, int mode)
@@ -1078,7 +1089,7 @@ __global__ void __launch_bounds__(256) k_quant(Params p, Workspace ws)
     int mode, part;
     task_mode((int)task, mode, part);
     const BlockMeta meta = ws.meta[b];
-    if (!(meta.valid & (1u << mode)) || (meta.flags & 3u)) return;   // integral blocks: k_quant_reg
+    if (!mode_active(meta, p, mode) || (meta.flags & 3u)) return;   // integral blocks: k_quant_reg
     if (part >= mode_tries(p, mode)) return;
     const ModeInfo &mi = kModes[mode];
     const int dim = mi.enc == ENC_NO_ALPHA ? 3 : 4;
@@ -1114,7 +1125,7 @@ __global__ void __launch_bounds__(256, 2) k_quant_reg(Params p, Workspace ws, in
     int mode, part;
     task_mode(task, mode, part);
     const BlockMeta meta = ws.meta[b];
-    if (!(meta.valid & (1u << mode)) || (meta.flags & 3u) != 2u) return;
+    if (!mode_active(meta, p, mode) || (meta.flags & 3u) != 2u) return;
     if (part >= mode_tries(p, mode)) return;
     const ModeInfo &mi = kModes[mode];
     const int ncl = 1 << mi.ib0;
@@ -1229,7 +1240,7 @@ __global__ void __launch_bounds__(256) k_shake(Params p, Workspace ws, const SpE
     const int slot = (int)(r / kShakeRanks), rank = (int)(r % kShakeRanks);
     const int mode = kSlotMode[slot];
     const BlockMeta meta = ws.meta[b];
-    if (!(meta.valid & (1u << mode)) || (meta.flags & 3u)) return;   // integral blocks: k_shake_wave
+    if (!mode_active(meta, p, mode) || (meta.flags & 3u)) return;   // integral blocks: k_shake_wave
     const ModeInfo &mi = kModes[mode];
     const int nparts = mode_tries(p, mode);   // partitions quantised and ranked
     if (rank >= mode_attempts(p, mode)) return;
@@ -1306,7 +1317,7 @@ __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, c
     wave_problem<NC>((int)(wid % WaveSet<NC>::count), slot, rank, subset);
     const int mode = kSlotMode[slot];
     const BlockMeta meta = ws.meta[b];
-    if (!(meta.valid & (1u << mode)) || (meta.flags & 3u) != 2u) return;
+    if (!mode_active(meta, p, mode) || (meta.flags & 3u) != 2u) return;
     const ModeInfo &mi = kModes[mode];
     const int nparts = mode_tries(p, mode);   // partitions quantised and ranked
     if (rank >= mode_attempts(p, mode)) return;
@@ -1412,7 +1423,7 @@ __global__ void __launch_bounds__(256, 2) k_dual_quant_reg(Params p, Workspace w
     int mode, rot, sel;
     dual_task(task, mode, rot, sel);
     const BlockMeta meta = ws.meta[b];
-    if (!(meta.valid & (1u << mode)) || (meta.flags & 3u) != 2u) return;
+    if (!mode_active(meta, p, mode) || (meta.flags & 3u) != 2u) return;
     const ModeInfo &mi = kModes[mode];
     const int ncl = 1 << (half ? (sel ? mi.ib0 : mi.ib1) : (sel ? mi.ib1 : mi.ib0));
     const float *tex = ws.tex + (size_t)b * 64;
@@ -1439,7 +1450,7 @@ __global__ void __launch_bounds__(256) k_dual_quant(Params p, Workspace ws)
     int mode, rot, sel;
     dual_task(task, mode, rot, sel);
     const BlockMeta meta = ws.meta[b];
-    if (!(meta.valid & (1u << mode)) || (meta.flags & 3u)) return;
+    if (!mode_active(meta, p, mode) || (meta.flags & 3u)) return;
     const ModeInfo &mi = kModes[mode];
     const int ibs[2] = {mi.ib0, mi.ib1};
     const float *tex = ws.tex + (size_t)b * 64;
@@ -1469,7 +1480,7 @@ __global__ void __launch_bounds__(256, 4) k_dual_wave(Params p, Workspace ws, co
     const int rot = task < 8 ? (int)(task >> 1) : (int)(task - 8);
     const int sel = task < 8 ? (int)(task & 1) : 0;
     const BlockMeta meta = ws.meta[b];
-    if (!(meta.valid & (1u << mode)) || (meta.flags & 3u) != 2u) return;
+    if (!mode_active(meta, p, mode) || (meta.flags & 3u) != 2u) return;
     const int ln = wv::lane();
     if (!dual_shaken(p, ws, b, (int)task)) {   // not shaken: never selected
         if (ln == 0) ws.dual[(size_t)b * kDualTasks + task].err[half] = 1.7976931348623157e308;
@@ -1524,7 +1535,7 @@ __global__ void __launch_bounds__(256) k_dual(Params p, Workspace ws, const SpEn
     const int rot = task < 8 ? (int)(task >> 1) : (int)(task - 8);
     const int sel = task < 8 ? (int)(task & 1) : 0;
     const BlockMeta meta = ws.meta[b];
-    if (!(meta.valid & (1u << mode)) || (meta.flags & 3u)) return;
+    if (!mode_active(meta, p, mode) || (meta.flags & 3u)) return;
     if (!dual_shaken(p, ws, b, (int)task)) {   // not shaken: never selected
         ws.dual[(size_t)b * kDualTasks + task].err[0] = 1.7976931348623157e308;
         ws.dual[(size_t)b * kDualTasks + task].err[1] = 1.7976931348623157e308;
@@ -1572,22 +1583,36 @@ __global__ void __launch_bounds__(256) k_dual(Params p, Workspace ws, const SpEn
 }
 
 // K4: mode selection in the reference's visiting order (CompressBlock :1400-1447)
-__global__ void __launch_bounds__(256) k_select(Params p, Workspace ws, uint4 *__restrict__ dst, double *__restrict__ err_out)
+// Mode visit order positions [k0, k1) of CompressBlock's loop; `resume`
+// continues from the state an earlier stage stored, k1 == 8 writes the block.
+__global__ void __launch_bounds__(256) k_select(Params p, Workspace ws, uint4 *__restrict__ dst, double *__restrict__ err_out,
+                                                int k0, int k1, int resume)
 {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= p.n) return;
-    const BlockMeta meta = ws.meta[b];
+    BlockMeta meta = ws.meta[b];
     const uint32_t out_id = p.first + b;
     if (meta.flags & 1u) {
-        dst[out_id] = make_uint4(0, 0, 0, 0);
-        if (err_out) err_out[out_id] = -1.0;
+        if (k1 == 8) {
+            dst[out_id] = make_uint4(0, 0, 0, 0);
+            if (err_out) err_out[out_id] = -1.0;
+        }
         return;
     }
     const int order[8] = {6, 4, 3, 1, 2, 0, 7, 5};
     double best = 1.7976931348623157e308;
     uint32_t bw[4] = {0, 0, 0, 0};
-    for (int k = 0; k < 8; ++k) {
+    if (resume) {
+        best = ws.best_err[b];
+        const uint4 v = ws.best_blk[b];
+        bw[0] = v.x;
+        bw[1] = v.y;
+        bw[2] = v.z;
+        bw[3] = v.w;
+    }
+    for (int k = k0; k < k1; ++k) {
         const int m = order[k];
+        if (meta.flags & 4u) break;
         if (!(meta.valid & (1u << m))) continue;
         double e;
         uint32_t w[4];
@@ -1645,7 +1670,16 @@ __global__ void __launch_bounds__(256) k_select(Params p, Workspace ws, uint4 *_
             best = e;
             for (int q = 0; q < 4; ++q) bw[q] = w[q];
         }
-        if (p.err_thr > 0 && best <= p.err_thr) break;   // CompressBlock :1440-1446
+        if (p.err_thr > 0 && best <= p.err_thr) {   // CompressBlock :1440-1446
+            meta.flags |= 4u;
+            break;
+        }
+    }
+    if (k1 < 8) {
+        ws.best_err[b] = best;
+        ws.best_blk[b] = make_uint4(bw[0], bw[1], bw[2], bw[3]);
+        ws.meta[b].flags = meta.flags;
+        return;
     }
     dst[out_id] = make_uint4(bw[0], bw[1], bw[2], bw[3]);
     if (err_out) err_out[out_id] = best;
@@ -1749,7 +1783,8 @@ static hipError_t get_state(uint32_t chunk, DeviceState *&out)
                           align_up(n * kQuantTasks * sizeof(double)) + align_up(n * kQuantTasks * sizeof(uint64_t)) +
                           align_up(n * kShakeSlots * kShakeRanks * sizeof(ShakeResult)) +
                           align_up(n * kDualTasks * sizeof(DualResult)) + align_up(n * kDualTasks * 2 * sizeof(uint64_t)) +
-                          align_up(n * kDualTasks * 2 * sizeof(double));
+                          align_up(n * kDualTasks * 2 * sizeof(double)) + align_up(n * sizeof(double)) +
+                          align_up(n * sizeof(uint4));
         e = hipMalloc(&st.ws_mem, sz);
         if (e != hipSuccess) return e;
         char *p = (char *)st.ws_mem;
@@ -1768,10 +1803,54 @@ static hipError_t get_state(uint32_t chunk, DeviceState *&out)
         st.ws.dqidx = (uint64_t *)p;
         p += align_up(n * kDualTasks * 2 * sizeof(uint64_t));
         st.ws.dqerr = (double *)p;
+        p += align_up(n * kDualTasks * 2 * sizeof(double));
+        st.ws.best_err = (double *)p;
+        p += align_up(n * sizeof(double));
+        st.ws.best_blk = (uint4 *)p;
         st.ws_blocks = chunk;
     }
     out = &st;
     return hipSuccess;
+}
+
+// K1-K3 for the modes of p.stage_mask (kernels return early for inactive work)
+static void run_modes(const Params &p, DeviceState *st, hipStream_t s)
+{
+    const uint32_t wg = 256;
+    const uint32_t sm = p.stage_mask;
+    const bool single = (sm & 0xCFu) != 0, dual = (sm & 0x30u) != 0;
+    if (single) {
+        const uint64_t nq = (uint64_t)p.n * kQuantTasks;
+        hipLaunchKernelGGL(k_quant, dim3((uint32_t)((nq + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws);
+        const uint64_t nq3 = (uint64_t)p.n * 208, nq4 = (uint64_t)p.n * 65;
+        if (sm & 0x0Fu)
+            hipLaunchKernelGGL(k_quant_reg<3>, dim3((uint32_t)((nq3 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, 0, 208);
+        if (sm & 0xC0u)
+            hipLaunchKernelGGL(k_quant_reg<4>, dim3((uint32_t)((nq4 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, 208, 65);
+        const uint64_t ns = (uint64_t)p.n * kShakeSlots * kShakeRanks;
+        hipLaunchKernelGGL(k_shake, dim3((uint32_t)((ns + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
+        if (sm & 0x03u) {
+            const uint64_t nw8 = (uint64_t)p.n * WaveSet<8>::count * 64;
+            hipLaunchKernelGGL(k_shake_wave<8>, dim3((uint32_t)((nw8 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
+        }
+        if (sm & 0x8Cu) {
+            const uint64_t nw4 = (uint64_t)p.n * WaveSet<4>::count * 64;
+            hipLaunchKernelGGL(k_shake_wave<4>, dim3((uint32_t)((nw4 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
+        }
+        if (sm & 0x40u) {
+            const uint64_t nw16 = (uint64_t)p.n * WaveSet<16>::count * 64;
+            hipLaunchKernelGGL(k_shake_wave<16>, dim3((uint32_t)((nw16 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
+        }
+    }
+    if (dual) {
+        const uint64_t ndq = (uint64_t)p.n * kDualTasks * 2;
+        hipLaunchKernelGGL(k_dual_quant, dim3((uint32_t)((ndq + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws);
+        hipLaunchKernelGGL(k_dual_quant_reg, dim3((uint32_t)((ndq + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws);
+        const uint64_t nd = (uint64_t)p.n * kDualTasks;
+        hipLaunchKernelGGL(k_dual, dim3((uint32_t)((nd + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
+        const uint64_t ndw = (uint64_t)p.n * kDualTasks * 2 * 64;
+        hipLaunchKernelGGL(k_dual_wave, dim3((uint32_t)((ndw + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
+    }
 }
 
 constexpr uint32_t kChunk = 65536;   // blocks per pipeline pass (~480 MB workspace)
@@ -1812,27 +1891,23 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
             hipLaunchKernelGGL(k_prep_image, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, *g, p, st->ws);
         else
             hipLaunchKernelGGL(k_prep_f32, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, blocks, p, st->ws);
-        const uint64_t nq = (uint64_t)p.n * kQuantTasks;
-        hipLaunchKernelGGL(k_quant, dim3((uint32_t)((nq + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws);
-        const uint64_t nq3 = (uint64_t)p.n * 208, nq4 = (uint64_t)p.n * 65;
-        hipLaunchKernelGGL(k_quant_reg<3>, dim3((uint32_t)((nq3 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, 0, 208);
-        hipLaunchKernelGGL(k_quant_reg<4>, dim3((uint32_t)((nq4 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, 208, 65);
-        const uint64_t ns = (uint64_t)p.n * kShakeSlots * kShakeRanks;
-        hipLaunchKernelGGL(k_shake, dim3((uint32_t)((ns + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
-        const uint64_t nw8 = (uint64_t)p.n * WaveSet<8>::count * 64;
-        hipLaunchKernelGGL(k_shake_wave<8>, dim3((uint32_t)((nw8 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
-        const uint64_t nw4 = (uint64_t)p.n * WaveSet<4>::count * 64;
-        hipLaunchKernelGGL(k_shake_wave<4>, dim3((uint32_t)((nw4 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
-        const uint64_t nw16 = (uint64_t)p.n * WaveSet<16>::count * 64;
-        hipLaunchKernelGGL(k_shake_wave<16>, dim3((uint32_t)((nw16 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
-        const uint64_t ndq = (uint64_t)p.n * kDualTasks * 2;
-        hipLaunchKernelGGL(k_dual_quant, dim3((uint32_t)((ndq + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws);
-        hipLaunchKernelGGL(k_dual_quant_reg, dim3((uint32_t)((ndq + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws);
-        const uint64_t nd = (uint64_t)p.n * kDualTasks;
-        hipLaunchKernelGGL(k_dual, dim3((uint32_t)((nd + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
-        const uint64_t ndw = (uint64_t)p.n * kDualTasks * 2 * 64;
-        hipLaunchKernelGGL(k_dual_wave, dim3((uint32_t)((ndw + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
-        hipLaunchKernelGGL(k_select, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, p, st->ws, (uint4 *)dst, err);
+        // err_thr > 0 (quality < 0.25): CompressBlock stops visiting modes once a
+        // block's best error is within the threshold, so the modes run one stage
+        // at a time in visit order and finished blocks drop out of later stages.
+        const bool staged = p.err_thr > 0;
+        const int order[8] = {6, 4, 3, 1, 2, 0, 7, 5};
+        const uint32_t valid_modes = o.bc7_mode_mask == 0 ? 0xCFu : o.bc7_mode_mask;
+        int resume = 0;
+        for (int k = 0; k < (staged ? 8 : 1); ++k) {
+            p.stage_mask = staged ? (1u << order[k]) : 0xFFu;
+            const bool last = !staged || k == 7;
+            const bool skip = staged && !(valid_modes & p.stage_mask);
+            if (skip && !last) continue;
+            if (!skip) run_modes(p, st, s);
+            hipLaunchKernelGGL(k_select, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, p, st->ws, (uint4 *)dst, err,
+                               staged ? k : 0, staged ? k + 1 : 8, resume);
+            resume = 1;
+        }
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
