@@ -68,6 +68,7 @@ int orc_bc7_shake_ramp(int clog, int bits, int p1, int p2, int i);
 double orc_bc7_opt_quant(const double *data4, int n, int ncl, int *index, int dim);
 /* decode one BC7 block to RGBA8 (for tolerance checks) */
 void orc_bc7_decode(const uint8_t blk[16], uint8_t rgba[64]);
+void orc_bc7_decode_n(const uint8_t *blk, size_t n, uint8_t *rgba);
 
 #ifdef __cplusplus
 }

@@ -1379,3 +1379,9 @@ void orc_bc7_decode(const uint8_t blk[16], uint8_t rgba[64])
         for (int c = 0; c < 4; ++c) rgba[i * 4 + c] = (uint8_t)px[c];
     }
 }
+
+/* decode n blocks (test helper for whole-image property checks) */
+void orc_bc7_decode_n(const uint8_t *blk, size_t n, uint8_t *rgba)
+{
+    for (size_t i = 0; i < n; ++i) orc_bc7_decode(blk + 16 * i, rgba + 64 * i);
+}

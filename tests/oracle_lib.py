@@ -47,6 +47,7 @@ def lib() -> ctypes.CDLL:
         _lib.orc_bc7_shake_ramp.argtypes = [ctypes.c_int] * 5
         _lib.orc_bc7_shake_ramp.restype = ctypes.c_int
         _lib.orc_bc7_decode.argtypes = [vp, vp]
+        _lib.orc_bc7_decode_n.argtypes = [vp, ctypes.c_size_t, vp]
     return _lib
 
 
@@ -121,8 +122,7 @@ def bc7_decode(blocks: np.ndarray) -> np.ndarray:
     """(n,16) uint8 -> (n,16,4) uint8 RGBA."""
     b = np.ascontiguousarray(blocks, dtype=np.uint8).reshape(-1, 16)
     out = np.zeros((b.shape[0], 16, 4), np.uint8)
-    for i in range(b.shape[0]):
-        lib().orc_bc7_decode(b[i].ctypes.data, out[i].ctypes.data)
+    lib().orc_bc7_decode_n(b.ctypes.data, b.shape[0], out.ctypes.data)
     return out
 
 

@@ -154,3 +154,34 @@ def test_bc7_quality_levels(gpu, quality):
         out = dst.cpu().numpy().reshape(-1, 16)
         ref = oracle_lib.encode_image_bc7(img, quality=quality)
         assert np.array_equal(out, ref), (quality, _mismatch_report(out, ref))
+
+
+def test_bc7_8k_whole_image_properties(gpu):
+    """Config 4 at full size (8192^2 G1): every block decodes, only modes 0-5
+    appear (opaque non-solid blocks drop 6/7, Q4), the decoded image is close
+    to the source, the per-block encoder errors are finite, and a sampled block
+    row is bit-identical to the oracle."""
+    import torch
+    n = 8192
+    src = synth.g1_torch(n, n, 1, seed=0x9E3779B9, device="cuda")
+    nb = (n // 4) * (n // 4)
+    dst = torch.empty(nb * 16, dtype=torch.uint8, device="cuda")
+    err = torch.empty(nb, dtype=torch.float64, device="cuda")
+    gic.encode_device(7, src, n, n, 1, 4, dst, gic.Options(), block_err=err)
+    torch.cuda.synchronize()
+    blocks = dst.cpu().numpy().reshape(-1, 16)
+    e = err.cpu().numpy()
+    assert np.isfinite(e).all() and (e >= 0).all()
+    low = blocks[:, 0].astype(np.int32)
+    assert (low != 0).all()
+    modes = np.log2(low & -low).astype(np.int32)          # BC7 mode = lowest set bit
+    assert modes.max() <= 5
+    dec = oracle_lib.bc7_decode(blocks)                    # (nb, 16, 4)
+    img = src.cpu().numpy()[0]
+    ref = img.reshape(n // 4, 4, n // 4, 4, 4).transpose(0, 2, 1, 3, 4).reshape(nb, 16, 4)
+    d = dec.astype(np.int32) - ref.astype(np.int32)
+    mse = float((d * d).sum(dtype=np.int64)) / d.size
+    psnr = 10 * np.log10(255.0 ** 2 / mse)
+    assert psnr > 40.0, psnr
+    row = oracle_lib.encode_image(7, img, first_row=1024, num_rows=1)
+    assert np.array_equal(blocks[1024 * (n // 4):1025 * (n // 4)], row)
