@@ -33,6 +33,7 @@ FMTS = {"bc1": 1, "bc4": 4, "bc5": 5, "bc7": 7}
 ALG_BYTES = {1: 72, 4: 24, 5: 48, 7: 80}   # source texels read + block written
 CHANNELS = {1: 4, 4: 1, 5: 2, 7: 4}
 HBM_PEAK_GBS = 8000.0                        # MI355X_MICROARCH.md chip table (spec)
+VALU_PEAK = 256 * 4 * 2.4e9 / 2              # wave64 VALU instructions/s: 256 CUs x 4 SIMDs, one per 2 cycles
 
 
 def parse():
@@ -263,10 +264,28 @@ def main():
         try:
             with open(tj) as f:
                 tr = json.load(f)
-            if tr.get("size") == size and tr.get("rows") == rows:
+            if tr.get("size") == size and tr.get("rows") == rows * 4:
                 traffic = tr.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
+
+    # VALU issue roofline of the same kernel: SQ_INSTS_VALU per launch from the
+    # committed PMC summary (tools/pmc_valu.sh + tools/valu_json.py, same
+    # workload) over this run's measured launch duration
+    valu = None
+    vj = os.path.join(ROOT, "profiles", f"valu_{args.format}.json")
+    if os.path.exists(vj):
+        try:
+            with open(vj) as f:
+                vr = json.load(f)
+            if vr.get("size") == size and vr.get("rows") == rows * 4:
+                rate = vr["valu_insts_per_launch"] / (kern_ms * 1e-3)
+                valu = {"bound": "valu", "achieved": round(rate / 1e12, 4), "peak": round(VALU_PEAK / 1e12, 4),
+                        "unit": "T wave-instr/s", "frac": round(rate / VALU_PEAK, 4),
+                        "insts_per_launch": vr["valu_insts_per_launch"], "kernel": vr.get("kernel", "")[:60],
+                        "source": os.path.relpath(vj, ROOT)}
+        except (OSError, ValueError, KeyError):
+            valu = None
 
     bc7 = None
     if fmt == 1 and args.bc7_rows != 0:
@@ -304,9 +323,12 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes,
-                         "note": "compute (VALU) bound; HBM fraction reported per BASELINE.json"},
+                         "note": "compute (VALU) bound; HBM fraction reported per BASELINE.json, the "
+                                 "binding VALU issue fraction in roofline.valu"},
             "cpu_baseline": cpu,
         }
+        if valu is not None:
+            line["roofline"]["valu"] = valu
         if gather_ms is not None:
             line["gather_ms"] = round(gather_ms, 3)
         if bc7 is not None:

@@ -53,13 +53,22 @@ static double g_sp_err[3][4][256][2][2][16];
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
 #ifdef ORC_STATS
 /* instrumentation build only (search-shape statistics for kernel design) */
-unsigned long long orc_stats[9][32];
+unsigned long long orc_stats[9][48];
 static __thread int st_mode = 8;
 #define ST(i, v) __atomic_fetch_add(&orc_stats[st_mode][i], (unsigned long long)(v), __ATOMIC_RELAXED)
 #define ST_MODE(m) (st_mode = (m))
 #else
 #define ST(i, v) ((void)0)
 #define ST_MODE(m) ((void)0)
+#endif
+
+#ifdef ORC_TRACE
+/* instrumentation build only (search-pruning studies): called per shaken
+ * partition rank (kind 0: err, per-subset errors) and per mode (kind 1) */
+void (*orc_bc7_trace)(int kind, int mode, int rank, int part, double err, const double *sub_err) = 0;
+#define TRACE(...) do { if (orc_bc7_trace) orc_bc7_trace(__VA_ARGS__); } while (0)
+#else
+#define TRACE(...) ((void)0)
 #endif
 
 static const double kLinW[5][16] = {
@@ -583,7 +592,11 @@ static double shake_window(double data[][4], int n, int *index_, int epo_code[2]
         const int Mi = max_index(index, n);
         int p0 = -1, q0 = -1;
         double err0 = DBL_MAX;
-        ST(6, 1); ST(16 + (Mi < 15 ? Mi : 15), 0);
+        ST(6, 1);
+#ifdef ORC_STATS
+        unsigned long long sigs[128][2];
+        int nsig = 0;
+#endif ST(16 + (Mi < 15 ? Mi : 15), 0);
         if (Mi == 0) {
             double t;
             if (alls) {
@@ -611,6 +624,19 @@ static double shake_window(double data[][4], int n, int *index_, int epo_code[2]
                 for (int k = 0; k < n; ++k) cidx[k] = index[k] * q + p;
                 ls_endpoints(data, cidx, n, last, dim, epa);
                 double err1 = DBL_MAX, ed[2][2][4]; ST(7, 1);
+#ifdef ORC_STATS
+                {
+                    unsigned long long sig = 0, sig1 = 0;
+                    for (int j = 0; j < dim; ++j)
+                        for (int i = 0; i < 2; ++i) {
+                            sig = sig * 256 + (unsigned)ep_floor(epa[i][j], mb[j], use_par, 0);
+                            sig1 = sig1 * 256 + (unsigned)ep_floor(epa[i][j], mb[j], use_par, 1);
+                        }
+                    int dup = 0;
+                    for (int k = 0; k < nsig; ++k) dup |= sigs[k][0] == sig && sigs[k][1] == sig1;
+                    if (dup) ST(12, 1); else { sigs[nsig][0] = sig; sigs[nsig++][1] = sig1; }
+                }
+#endif
                 int epo1[2][4], best2[2][2][2][4];
                 for (int j = 0; j < dim; ++j) {
                     const int rr = use_par ? 2 : 1;
@@ -720,6 +746,10 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
         const int Mi = max_index(index, n);
         int p0 = -1, q0 = -1, idx2[16] = {0}, epo2[2][4] = {{0}};
         double err2 = DBL_MAX; ST(1, 1); ST(16 + (Mi < 15 ? Mi : 15), 1);
+#ifdef ORC_STATS
+        unsigned long long sigs[128][2];
+        int nsig = 0;
+#endif
         if (Mi == 0) {
             double t, o2[16][4];
             int epo0[2][4] = {{0}};
@@ -747,6 +777,19 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
                 double epa[2][4], err1 = DBL_MAX; ST(2, 1);
                 for (int k = 0; k < n; ++k) cidx[k] = index[k] * q + p;
                 ls_endpoints(data, cidx, n, last, dim, epa);
+#ifdef ORC_STATS
+                { /* expansions whose floor codes repeat an earlier expansion's */
+                    unsigned long long sig = 0, sig1 = 0;
+                    for (int j = 0; j < dim; ++j)
+                        for (int i = 0; i < 2; ++i) {
+                            sig = sig * 256 + (unsigned)ep_floor(epa[i][j], bits[j], use_par, 0);
+                            sig1 = sig1 * 256 + (unsigned)ep_floor(epa[i][j], bits[j], use_par, 1);
+                        }
+                    int dup = 0;
+                    for (int k = 0; k < nsig; ++k) dup |= sigs[k][0] == sig && sigs[k][1] == sig1;
+                    if (dup) ST(15, 1); else { sigs[nsig][0] = sig; sigs[nsig++][1] = sig1; }
+                }
+#endif
                 for (int odd = 0; odd <= use_par; ++odd)
                     for (int flip = 0; flip <= bcc; ++flip) {
                         int epi[2][4][2]; ST(3, 1); ST(4, n);
@@ -759,33 +802,11 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
                                                      : (1 << use_par)) &
                                                 (~use_par);
                             }
-#ifdef ORC_STATS
-                        { /* pass lower bound: per texel, channels choose options independently */
-                            double lb = 0;
-                            for (int i = 0; i < n; ++i) {
-                                double best = DBL_MAX;
-                                for (int c = 0; c < nc; ++c) {
-                                    double t = 0;
-                                    for (int j = 0; j < dim; ++j) {
-                                        double bj = DBL_MAX;
-                                        for (int o = 0; o < 4; ++o) {
-                                            double rv = shake_ramp(clog, bits[j], epi[0][j][o & 1], epi[1][j][o >> 1], c);
-                                            double dv = (rv - data[i][j]) * (rv - data[i][j]);
-                                            bj = dv < bj ? dv : bj;
-                                        }
-                                        t += bj;
-                                    }
-                                    best = t < best ? t : best;
-                                }
-                                lb += best;
-                            }
-                            const double thr = err1 < err2 ? err1 : err2;
-                            ST(12, 1);
-                            if (lb >= thr) ST(13, 1);
-                            if (lb >= err1) ST(14, 1);
-                        }
-#endif
                         /* 64-corner Gray-code walk :1273-1341; evaluated per corner */
+#ifdef ORC_STATS
+                        double te_[64][16];
+                        const double thr_ = err1 < err2 ? err1 : err2;
+#endif
                         int s = 0;
                         for (int p1 = 0; p1 < 64; ++p1) {
                             const int g = p1 & (-p1);
@@ -812,6 +833,9 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
                                 }
                                 idx0[i] = ci;
                                 err0 += cmin;
+#ifdef ORC_STATS
+                                te_[p1][i] = cmin;
+#endif
                             }
                             if (err0 < err1) {
                                 for (int i = 0; i < n; ++i) idx1[i] = idx0[i];
@@ -819,6 +843,32 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
                                 s1 = s;
                             }
                         }
+#ifdef ORC_STATS
+                        { /* GPU cut simulation: texels processed before every corner reaches thr */
+                            int ord[2][16];
+                            for (int i = 0; i < n; ++i) ord[0][i] = ord[1][i] = i;
+                            double dm[16];
+                            for (int i = 0; i < n; ++i) {
+                                dm[i] = 0;
+                                for (int k = 0; k < dim; ++k) dm[i] += (data[i][k] - mean[k]) * (data[i][k] - mean[k]);
+                            }
+                            for (int i = 1; i < n; ++i) /* stable insertion sort, descending */
+                                for (int k = i; k > 0 && dm[ord[1][k]] > dm[ord[1][k - 1]]; --k) {
+                                    int t = ord[1][k]; ord[1][k] = ord[1][k - 1]; ord[1][k - 1] = t;
+                                }
+                            ST(32, 1); ST(35, n);
+                            for (int o = 0; o < 2; ++o) {
+                                double part[64] = {0};
+                                int used = n;
+                                for (int m = 0; m < n; ++m) {
+                                    int all = 1;
+                                    for (int c = 0; c < 64; ++c) { part[c] += te_[c][ord[o][m]]; all &= part[c] >= thr_; }
+                                    if ((m & 1) && all) { used = m + 1; break; }
+                                }
+                                ST(33 + o, used);
+                            }
+                        }
+#endif
                         /* Q6: rebuilt from the global s1 and this pass's ranges */
                         for (int j = 0; j < dim; ++j) {
                             epo1[0][j] = epi[0][j][(s1 >> (2 * j)) & 1];
@@ -1046,14 +1096,15 @@ static double single_index(bc7_enc *e, double in[16][4], uint8_t out[16], int mo
     memset(epo_code, 0, sizeof(epo_code));
     memset(best_ep, 0, sizeof(best_ep));
     for (unsigned i = 0; i < attempts; ++i) {
-        double err = 0;
+        double err = 0, sub_err[3] = {0, 0, 0};
         const int part = e->sorted[i];
         split_subsets(part, in, sub, cnt, mi->subsets, dim);
         for (int s = 0; s < mi->subsets; ++s) {
             if (!cnt[s]) continue;
             if (e->max_range > e->shake_thr || dim != 3) {
-                err += shake_window(sub[s], cnt[s], e->stored[part][s], epo_code[s], (int)shake,
-                                    e->clusters[0] - 1, bits[3], dim);
+                sub_err[s] = shake_window(sub[s], cnt[s], e->stored[part][s], epo_code[s], (int)shake,
+                                          e->clusters[0] - 1, bits[3], dim);
+                err += sub_err[s];
             } else {
                 int tidx[16], tepo[2][4];
                 double te[2];
@@ -1071,9 +1122,11 @@ static double single_index(bc7_enc *e, double in[16][4], uint8_t out[16], int mo
                         epo_code[s][1][k] = tepo[1][k];
                     }
                 }
+                sub_err[s] = te[1];
                 err += te[1];
             }
         }
+        TRACE(0, mode, (int)i, part, err, sub_err);
         if (err < best_err) {
             best_part = (unsigned)part;
             for (int s = 0; s < mi->subsets; ++s) {
@@ -1282,6 +1335,7 @@ double orc_bc7_block(const float inN[64], uint8_t mode_mask, int src_has_alpha, 
         mode_setup(e, m);
         double err = kModes[m].enc != ENC_SEPARATE ? single_index(e, in, tmp, m) : dual_index(e, in, tmp, m);
         if (e->unsupported) return -1.0;
+        TRACE(1, m, -1, -1, err, (const double *)0);
         if (err < best) {
             memcpy(out, tmp, 16);
             best = err;
