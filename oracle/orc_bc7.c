@@ -596,7 +596,8 @@ static double shake_window(double data[][4], int n, int *index_, int epo_code[2]
 #ifdef ORC_STATS
         unsigned long long sigs[128][2];
         int nsig = 0;
-#endif ST(16 + (Mi < 15 ? Mi : 15), 0);
+#endif
+        ST(16 + (Mi < 15 ? Mi : 15), 0);
         if (Mi == 0) {
             double t;
             if (alls) {

@@ -1,0 +1,14 @@
+# rocprofv3 kernel stats of a short BC7 bench: bash tools/prof_kernels.sh ROWS OUTNAME
+set -o pipefail
+ROWS=${1:-64}; OUT=${2:-prof_k}
+R=${GRAFT_REPO_ROOT:-$PWD}
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/$OUT -o run -- python3 $R/bench.py --format bc7 --rows $ROWS --steps 1 --warmup 1 --no-cpu > $R/gpurun_out/$OUT.log 2>&1
+rc=$?
+f=$(find $R/gpurun_out/$OUT -name "*kernel_stats.csv" | head -1)
+python3 -c "
+import csv,sys
+rows=list(csv.DictReader(open('$f')))
+for r in rows[:12]: print(r['Name'][:60], r['Calls'], r['TotalDurationNs'], r['Percentage'])
+"
+exit $rc
