@@ -5,10 +5,5 @@ R=${GRAFT_REPO_ROOT:-$PWD}
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/$OUT -o run -- python3 $R/bench.py --format bc7 --rows $ROWS --steps 1 --warmup 1 --no-cpu > $R/gpurun_out/$OUT.log 2>&1
 rc=$?
-f=$(find $R/gpurun_out/$OUT -name "*kernel_stats.csv" | head -1)
-python3 -c "
-import csv,sys
-rows=list(csv.DictReader(open('$f')))
-for r in rows[:12]: print(r['Name'][:60], r['Calls'], r['TotalDurationNs'], r['Percentage'])
-"
+python3 $R/tools/kstats.py $(find $R/gpurun_out/$OUT -name "*.db" | head -1)
 exit $rc
