@@ -742,6 +742,10 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
     for (int k = 0; k < n; ++k) index[k] = index_[k];
     const int alls = all_same(data, n, dim);
     mean_of(data, mean, n, dim);
+#ifdef ORC_STATS
+    unsigned long long psig[512];
+    int npsig = 0;
+#endif
     do {
         collapse(index, n);
         const int Mi = max_index(index, n);
@@ -805,6 +809,15 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
                             }
                         /* 64-corner Gray-code walk :1273-1341; evaluated per corner */
 #ifdef ORC_STATS
+                        { /* passes whose endpoint ranges repeat an earlier pass of this call */
+                            unsigned long long ps = 0;
+                            for (int j = 0; j < dim; ++j)
+                                for (int i = 0; i < 2; ++i) ps = ps * 256 + (unsigned)epi[i][j][0];
+                            int dup = 0;
+                            for (int k = 0; k < npsig; ++k) dup |= psig[k] == ps;
+                            ST(36, 1);
+                            if (dup) ST(37, 1); else if (npsig < 512) psig[npsig++] = ps;
+                        }
                         double te_[64][16];
                         const double thr_ = err1 < err2 ? err1 : err2;
 #endif
