@@ -1738,12 +1738,19 @@ static void build_sp_table(std::vector<SpEntry> &tab)
                         }
 }
 
+// Per-device state: the single-point table, and two chunk workspaces with two
+// internal streams, so that consecutive chunks run concurrently (one chunk's
+// quantiser beside the other's shakers, and each launch's tail beside the
+// other stream's work) -- chunks are independent, each stays in order on its
+// own stream.
 struct DeviceState {
     int device = -1;
     SpEntry *sp = nullptr;
-    void *ws_mem = nullptr;
-    uint32_t ws_blocks = 0;
-    Workspace ws{};
+    void *ws_mem[2] = {nullptr, nullptr};
+    uint32_t ws_blocks[2] = {0, 0};
+    Workspace ws[2]{};
+    hipStream_t lane[2] = {nullptr, nullptr};
+    hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
 };
 
 static std::mutex g_state_lock;
@@ -1751,7 +1758,7 @@ static DeviceState g_states[64];
 
 static size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
 
-static hipError_t get_state(uint32_t chunk, DeviceState *&out)
+static hipError_t get_state(uint32_t chunk, int nsets, DeviceState *&out)
 {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -1774,10 +1781,11 @@ static hipError_t get_state(uint32_t chunk, DeviceState *&out)
         if (e != hipSuccess) return e;
         st.device = dev;
     }
-    if (st.ws_blocks < chunk) {
-        if (st.ws_mem) (void)hipFree(st.ws_mem);
-        st.ws_mem = nullptr;
-        st.ws_blocks = 0;
+    for (int k = 0; k < nsets; ++k) {
+        if (st.ws_blocks[k] >= chunk) continue;
+        if (st.ws_mem[k]) (void)hipFree(st.ws_mem[k]);
+        st.ws_mem[k] = nullptr;
+        st.ws_blocks[k] = 0;
         const size_t n = chunk;
         const size_t sz = align_up(n * 64 * sizeof(float)) + align_up(n * sizeof(BlockMeta)) +
                           align_up(n * kQuantTasks * sizeof(double)) + align_up(n * kQuantTasks * sizeof(uint64_t)) +
@@ -1785,71 +1793,81 @@ static hipError_t get_state(uint32_t chunk, DeviceState *&out)
                           align_up(n * kDualTasks * sizeof(DualResult)) + align_up(n * kDualTasks * 2 * sizeof(uint64_t)) +
                           align_up(n * kDualTasks * 2 * sizeof(double)) + align_up(n * sizeof(double)) +
                           align_up(n * sizeof(uint4));
-        e = hipMalloc(&st.ws_mem, sz);
+        e = hipMalloc(&st.ws_mem[k], sz);
         if (e != hipSuccess) return e;
-        char *p = (char *)st.ws_mem;
-        st.ws.tex = (float *)p;
+        Workspace &w = st.ws[k];
+        char *p = (char *)st.ws_mem[k];
+        w.tex = (float *)p;
         p += align_up(n * 64 * sizeof(float));
-        st.ws.meta = (BlockMeta *)p;
+        w.meta = (BlockMeta *)p;
         p += align_up(n * sizeof(BlockMeta));
-        st.ws.qerr = (double *)p;
+        w.qerr = (double *)p;
         p += align_up(n * kQuantTasks * sizeof(double));
-        st.ws.qidx = (uint64_t *)p;
+        w.qidx = (uint64_t *)p;
         p += align_up(n * kQuantTasks * sizeof(uint64_t));
-        st.ws.shk = (ShakeResult *)p;
+        w.shk = (ShakeResult *)p;
         p += align_up(n * kShakeSlots * kShakeRanks * sizeof(ShakeResult));
-        st.ws.dual = (DualResult *)p;
+        w.dual = (DualResult *)p;
         p += align_up(n * kDualTasks * sizeof(DualResult));
-        st.ws.dqidx = (uint64_t *)p;
+        w.dqidx = (uint64_t *)p;
         p += align_up(n * kDualTasks * 2 * sizeof(uint64_t));
-        st.ws.dqerr = (double *)p;
+        w.dqerr = (double *)p;
         p += align_up(n * kDualTasks * 2 * sizeof(double));
-        st.ws.best_err = (double *)p;
+        w.best_err = (double *)p;
         p += align_up(n * sizeof(double));
-        st.ws.best_blk = (uint4 *)p;
-        st.ws_blocks = chunk;
+        w.best_blk = (uint4 *)p;
+        st.ws_blocks[k] = chunk;
+    }
+    if (nsets > 1 && !st.lane[0]) {
+        for (int k = 0; k < 2; ++k) {
+            e = hipStreamCreateWithFlags(&st.lane[k], hipStreamNonBlocking);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&st.ev_join[k], hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+        e = hipEventCreateWithFlags(&st.ev_fork, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
     }
     out = &st;
     return hipSuccess;
 }
 
 // K1-K3 for the modes of p.stage_mask (kernels return early for inactive work)
-static void run_modes(const Params &p, DeviceState *st, hipStream_t s)
+static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, hipStream_t s)
 {
     const uint32_t wg = 256;
     const uint32_t sm = p.stage_mask;
     const bool single = (sm & 0xCFu) != 0, dual = (sm & 0x30u) != 0;
     if (single) {
         const uint64_t nq = (uint64_t)p.n * kQuantTasks;
-        hipLaunchKernelGGL(k_quant, dim3((uint32_t)((nq + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws);
+        hipLaunchKernelGGL(k_quant, dim3((uint32_t)((nq + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
         const uint64_t nq3 = (uint64_t)p.n * 208, nq4 = (uint64_t)p.n * 65;
         if (sm & 0x0Fu)
-            hipLaunchKernelGGL(k_quant_reg<3>, dim3((uint32_t)((nq3 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, 0, 208);
+            hipLaunchKernelGGL(k_quant_reg<3>, dim3((uint32_t)((nq3 + wg - 1) / wg)), dim3(wg), 0, s, p, ws, 0, 208);
         if (sm & 0xC0u)
-            hipLaunchKernelGGL(k_quant_reg<4>, dim3((uint32_t)((nq4 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, 208, 65);
+            hipLaunchKernelGGL(k_quant_reg<4>, dim3((uint32_t)((nq4 + wg - 1) / wg)), dim3(wg), 0, s, p, ws, 208, 65);
         const uint64_t ns = (uint64_t)p.n * kShakeSlots * kShakeRanks;
-        hipLaunchKernelGGL(k_shake, dim3((uint32_t)((ns + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
+        hipLaunchKernelGGL(k_shake, dim3((uint32_t)((ns + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
         if (sm & 0x03u) {
             const uint64_t nw8 = (uint64_t)p.n * WaveSet<8>::count * 64;
-            hipLaunchKernelGGL(k_shake_wave<8>, dim3((uint32_t)((nw8 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
+            hipLaunchKernelGGL(k_shake_wave<8>, dim3((uint32_t)((nw8 + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
         }
         if (sm & 0x8Cu) {
             const uint64_t nw4 = (uint64_t)p.n * WaveSet<4>::count * 64;
-            hipLaunchKernelGGL(k_shake_wave<4>, dim3((uint32_t)((nw4 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
+            hipLaunchKernelGGL(k_shake_wave<4>, dim3((uint32_t)((nw4 + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
         }
         if (sm & 0x40u) {
             const uint64_t nw16 = (uint64_t)p.n * WaveSet<16>::count * 64;
-            hipLaunchKernelGGL(k_shake_wave<16>, dim3((uint32_t)((nw16 + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
+            hipLaunchKernelGGL(k_shake_wave<16>, dim3((uint32_t)((nw16 + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
         }
     }
     if (dual) {
         const uint64_t ndq = (uint64_t)p.n * kDualTasks * 2;
-        hipLaunchKernelGGL(k_dual_quant, dim3((uint32_t)((ndq + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws);
-        hipLaunchKernelGGL(k_dual_quant_reg, dim3((uint32_t)((ndq + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws);
+        hipLaunchKernelGGL(k_dual_quant, dim3((uint32_t)((ndq + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
+        hipLaunchKernelGGL(k_dual_quant_reg, dim3((uint32_t)((ndq + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
         const uint64_t nd = (uint64_t)p.n * kDualTasks;
-        hipLaunchKernelGGL(k_dual, dim3((uint32_t)((nd + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
+        hipLaunchKernelGGL(k_dual, dim3((uint32_t)((nd + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
         const uint64_t ndw = (uint64_t)p.n * kDualTasks * 2 * 64;
-        hipLaunchKernelGGL(k_dual_wave, dim3((uint32_t)((ndw + wg - 1) / wg)), dim3(wg), 0, s, p, st->ws, st->sp);
+        hipLaunchKernelGGL(k_dual_wave, dim3((uint32_t)((ndw + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
     }
 }
 
@@ -1859,10 +1877,20 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
                              double *err, hipStream_t s)
 {
     const uint32_t chunk = total < kChunk ? total : kChunk;
+    const int nsets = total > chunk ? 2 : 1;
     DeviceState *st = nullptr;
-    hipError_t e = get_state(chunk, st);
+    hipError_t e = get_state(chunk, nsets, st);
     if (e != hipSuccess) return e;
-    for (uint32_t first = 0; first < total; first += chunk) {
+    if (nsets > 1) {   // fork: both lanes start after the caller's prior work
+        e = hipEventRecord(st->ev_fork, s);
+        for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipStreamWaitEvent(st->lane[k], st->ev_fork, 0);
+        if (e != hipSuccess) return e;
+    }
+    const hipStream_t caller = s;
+    uint32_t ci = 0;
+    for (uint32_t first = 0; first < total; first += chunk, ++ci) {
+        const Workspace &ws = st->ws[nsets > 1 ? (ci & 1) : 0];
+        s = nsets > 1 ? st->lane[ci & 1] : caller;
         Params p;
         p.mode_mask = o.bc7_mode_mask;
         p.colour_restrict = o.colour_restrict;
@@ -1888,9 +1916,9 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
         }
         const uint32_t wg = 256;
         if (g)
-            hipLaunchKernelGGL(k_prep_image, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, *g, p, st->ws);
+            hipLaunchKernelGGL(k_prep_image, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, *g, p, ws);
         else
-            hipLaunchKernelGGL(k_prep_f32, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, blocks, p, st->ws);
+            hipLaunchKernelGGL(k_prep_f32, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, blocks, p, ws);
         // err_thr > 0 (quality < 0.25): CompressBlock stops visiting modes once a
         // block's best error is within the threshold, so the modes run one stage
         // at a time in visit order and finished blocks drop out of later stages.
@@ -1903,15 +1931,21 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
             const bool last = !staged || k == 7;
             const bool skip = staged && !(valid_modes & p.stage_mask);
             if (skip && !last) continue;
-            if (!skip) run_modes(p, st, s);
-            hipLaunchKernelGGL(k_select, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, p, st->ws, (uint4 *)dst, err,
+            if (!skip) run_modes(p, ws, st->sp, s);
+            hipLaunchKernelGGL(k_select, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, p, ws, (uint4 *)dst, err,
                                staged ? k : 0, staged ? k + 1 : 8, resume);
             resume = 1;
         }
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    return hipSuccess;
+    if (nsets > 1) {   // join: the caller's stream waits for both lanes
+        for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+            e = hipEventRecord(st->ev_join[k], st->lane[k]);
+            if (e == hipSuccess) e = hipStreamWaitEvent(caller, st->ev_join[k], 0);
+        }
+    }
+    return e;
 }
 
 }  // namespace bc7
