@@ -23,6 +23,7 @@
 // The per-block workspace (~7 KB) lives in HBM between phases.
 
 #include <vector>
+#include <cstdlib>
 #include <mutex>
 
 #include "gic_common.h"
@@ -1877,7 +1878,10 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
                              double *err, hipStream_t s)
 {
     const uint32_t chunk = total < kChunk ? total : kChunk;
-    const int nsets = total > chunk ? 2 : 1;
+    // GIC_BC7_SINGLE_STREAM=1: every chunk on the caller's stream (per-kernel
+    // profiles then attribute time without the two lanes' overlap)
+    static const bool single_stream = getenv("GIC_BC7_SINGLE_STREAM") && atoi(getenv("GIC_BC7_SINGLE_STREAM"));
+    const int nsets = (total > chunk && !single_stream) ? 2 : 1;
     DeviceState *st = nullptr;
     hipError_t e = get_state(chunk, nsets, st);
     if (e != hipSuccess) return e;
