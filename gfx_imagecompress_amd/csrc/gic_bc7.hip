@@ -1306,6 +1306,18 @@ __device__ __forceinline__ void wave_problem(int id, int &slot, int &rank, int &
     }
 }
 
+// a rank's subset result, following a repeated-problem reference (k_shake_wave)
+__device__ __forceinline__ const ShakeResult &shake_ref(const ShakeResult *shk, int r, int s)
+{
+    const double e = shk[r].err[s];
+    return e < 0 ? shk[(int)(-1.0 - e) >> 2] : shk[r];
+}
+__device__ __forceinline__ int shake_sub(const ShakeResult *shk, int r, int s)
+{
+    const double e = shk[r].err[s];
+    return e < 0 ? ((int)(-1.0 - e) & 3) : s;
+}
+
 // K2 (waves): one wavefront per (block, mode, rank, subset) shake problem of
 // an integral block
 template <int NC>
@@ -1324,11 +1336,10 @@ __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, c
     if (rank >= mode_attempts(p, mode)) return;
     // stable rank of every partition, lane = partition (sortProjection order)
     const int ln = wv::lane();
-    int part;
+    int part, rk = 0;
     {
         const double *qe = ws.qerr + (size_t)b * kQuantTasks + kSlotBase[slot];
         const double v = ln < nparts ? qe[ln] : 0.0;
-        int rk = 0;
         for (int o = 0; o < nparts; ++o) {
             const double w = wv::bcast_d(v, o);
             rk += (w - v < 0 || (!(w - v > 0) && !(w - v < 0) && o < ln)) ? 1 : 0;
@@ -1342,6 +1353,36 @@ __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, c
     // gather the subset: lane L < n holds the L-th texel of the subset
     uint32_t mask = 0;
     for (int t = 0; t < 16; ++t) mask |= ((int)shape_of(mi.subsets, part, t) == subset ? 1u : 0u) << t;
+    ShakeResult &res = ws.shk[((size_t)b * kShakeSlots + slot) * kShakeRanks + rank];
+    // Repeated problem (exact): three-subset shapes share subset masks, and a
+    // subset's quantiser indices and shake depend only on its texels, so when a
+    // lower rank of this mode shakes a subset with the same mask the result is
+    // identical.  Only a reference (-1 - (rank*4 + subset)) is stored; k_select
+    // reads the first occurrence.  (Two-subset shapes never repeat a mask.)
+    if (mi.subsets == 3) {
+        int key = 0x7fffffff;
+        if (ln < nparts && rk < rank) {
+            const uint32_t sh = dShape3[ln];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const uint32_t x = sh ^ (0x55555555u * (uint32_t)j);
+                uint32_t z = ~(x | (x >> 1)) & 0x55555555u;   // bit 2t: texel t in subset j
+                z = (z | (z >> 1)) & 0x33333333u;
+                z = (z | (z >> 2)) & 0x0f0f0f0fu;
+                z = (z | (z >> 4)) & 0x00ff00ffu;
+                z = (z | (z >> 8)) & 0x0000ffffu;
+                if (z == mask) key = wv::imin(key, rk * 4 + j);
+            }
+        }
+        key = wv::wmin(key);
+        if (key != 0x7fffffff) {
+            if (ln == 0) {
+                if (subset == 0) res.part = (uint32_t)part;
+                res.err[subset] = -1.0 - (double)key;
+            }
+            return;
+        }
+    }
     const int n = __popc(mask);
     int src = 0;
     {
@@ -1367,7 +1408,6 @@ __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, c
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) ti |= __shfl_xor(ti, o);
     if (ln == 0) {
-        ShakeResult &res = ws.shk[((size_t)b * kShakeSlots + slot) * kShakeRanks + rank];
         if (subset == 0) res.part = (uint32_t)part;
         res.err[subset] = e;
         res.idx[subset] = ti;
@@ -1652,10 +1692,10 @@ __global__ void __launch_bounds__(256) k_select(Params p, Workspace ws, uint4 *_
             const int ns = kModes[m].subsets;
             int bi = 0;
             double be = 1.7976931348623157e308;
+            const ShakeResult *shk = ws.shk + ((size_t)b * kShakeSlots + slot) * kShakeRanks;
             for (int r = 0; r < attempts; ++r) {
-                const ShakeResult &sr = ws.shk[((size_t)b * kShakeSlots + slot) * kShakeRanks + r];
                 double v = 0;
-                for (int s = 0; s < ns; ++s) v += sr.err[s];
+                for (int s = 0; s < ns; ++s) v += shake_ref(shk, r, s).err[shake_sub(shk, r, s)];
                 if (v < be) {
                     be = v;
                     bi = r;
@@ -1663,9 +1703,16 @@ __global__ void __launch_bounds__(256) k_select(Params p, Workspace ws, uint4 *_
                 if (p.err_thr > 0 && be <= p.err_thr) break;   // :837-843
             }
             e = be;
-            const ShakeResult &sr = ws.shk[((size_t)b * kShakeSlots + slot) * kShakeRanks + bi];
-            const uint64_t tidx = sr.idx[0] | (ns > 1 ? sr.idx[1] : 0ull) | (ns > 2 ? sr.idx[2] : 0ull);
-            pack_single(m, (int)sr.part, sr.ep, tidx, w);
+            uint8_t ep[3][2][4];
+            uint64_t tidx = 0;
+            for (int s = 0; s < ns; ++s) {   // repeated subsets: their first occurrence
+                const ShakeResult &src = shake_ref(shk, bi, s);
+                const int ss = shake_sub(shk, bi, s);
+                tidx |= src.idx[ss];
+                for (int k = 0; k < 2; ++k)
+                    for (int c = 0; c < 4; ++c) ep[s][k][c] = src.ep[ss][k][c];
+            }
+            pack_single(m, (int)shk[bi].part, ep, tidx, w);
         }
         if (e < best) {
             best = e;
