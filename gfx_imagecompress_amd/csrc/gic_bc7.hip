@@ -58,6 +58,12 @@ constexpr int kQuantTasks = 273;   // m0:16, m1:64, m2:64, m3:64, m6:1, m7:64
 constexpr int kShakeSlots = 6;     // modes 0,1,2,3,6,7
 constexpr int kShakeRanks = 8;
 constexpr int kDualTasks = 12;     // mode 4: 4 rot x 2 sel, mode 5: 4 rot
+// Distinct (subset mask, cluster count) problems among the subsets of modes
+// 0-3's partitions (k_quant_sub): 150 with 8 clusters, 242 with 4, of 496.
+constexpr int kUMax = 496;
+__constant__ uint32_t dUProb[kUMax];      // mask | log2(clusters) << 16
+__constant__ uint32_t dUMinPart[kUMax];   // byte m: lowest partition of mode m using it, 0xFF = none
+__constant__ uint16_t dTaskSub[208][3];   // task (modes 0-3) x subset -> problem, 0xFFFF = no subset
 __constant__ int kSlotMode[6] = {0, 1, 2, 3, 6, 7};
 __constant__ int kSlotBase[6] = {0, 16, 80, 144, 208, 209};
 
@@ -103,6 +109,8 @@ struct Workspace {
     double *dqerr;         // [n][12][2] their optQuantAnD_d errors (quality <= 0.7 gating)
     double *best_err;      // [n] running best over the modes of earlier stages
     uint4 *best_blk;       // [n] its packed block
+    double *uerr;          // [n][kUMax] optQuantAnD_d error of each distinct subset problem (modes 0-3)
+    uint64_t *uidx;        // [n][kUMax] its indices, 4 bits per texel of the subset (texel order)
 };
 
 __device__ __forceinline__ int expand_code(int bits, int v) { return (v << (8 - bits)) | (v >> (2 * bits - 8)); }
@@ -1115,6 +1123,70 @@ __global__ void __launch_bounds__(256) k_quant(Params p, Workspace ws)
     ws.qidx[(size_t)b * kQuantTasks + task] = tidx;
 }
 
+// K1a (integral blocks, modes 0-3): optQuantAnD_d once per distinct subset
+// problem.  A subset's quantiser result depends only on its texels (mask, in
+// texel order) and cluster count, and the partition tables repeat masks (21 %
+// of modes 0-3's subset problems), so each distinct one is solved once and
+// k_quant_gather sums the per-partition errors in subset order, exactly as the
+// per-partition loop of CompressSingleIndexBlock (:582-641) does.
+__global__ void __launch_bounds__(256, 2) k_quant_sub(Params p, Workspace ws, int nu)
+{
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t b = gid / (uint32_t)nu;
+    const int u = (int)(gid % (uint32_t)nu);
+    if (b >= p.n) return;
+    const BlockMeta meta = ws.meta[b];
+    if ((meta.flags & 3u) != 2u) return;
+    const uint32_t mp = dUMinPart[u];
+    bool need = false;
+    for (int m = 0; m < 4; ++m) {
+        const uint32_t mpart = (mp >> (8 * m)) & 0xFFu;
+        need = need || (mpart != 0xFFu && mode_active(meta, p, m) && (int)mpart < mode_tries(p, m));
+    }
+    if (!need) return;
+    const float *tex = ws.tex + (size_t)b * 64;
+    uint32_t px[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const float4 v = *reinterpret_cast<const float4 *>(tex + i * 4);
+        px[i] = (uint32_t)v.x | ((uint32_t)v.y << 8) | ((uint32_t)v.z << 16) | ((uint32_t)v.w << 24);
+    }
+    const uint32_t pr = dUProb[u];
+    const uint32_t mask = pr & 0xFFFFu;
+    int idx[16];
+    const double err = opt_quant_mask<3>(px, mask, 1 << (pr >> 16), idx);
+    uint64_t tidx = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if ((mask >> i) & 1u) tidx |= (uint64_t)(idx[i] & 15) << (4 * i);
+    ws.uerr[(size_t)b * kUMax + u] = err;
+    ws.uidx[(size_t)b * kUMax + u] = tidx;
+}
+
+// K1b: per-partition errors and indices of modes 0-3 from the subset problems
+__global__ void __launch_bounds__(256) k_quant_gather(Params p, Workspace ws)
+{
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t b = gid / 208u;
+    const int task = (int)(gid % 208u);
+    if (b >= p.n) return;
+    int mode, part;
+    task_mode(task, mode, part);
+    const BlockMeta meta = ws.meta[b];
+    if (!mode_active(meta, p, mode) || (meta.flags & 3u) != 2u) return;
+    if (part >= mode_tries(p, mode)) return;
+    double err = 0.;
+    uint64_t tidx = 0;
+    for (int sub = 0; sub < 3; ++sub) {
+        const int u = dTaskSub[task][sub];
+        if (u == 0xFFFF) break;
+        err += ws.uerr[(size_t)b * kUMax + u];
+        tidx |= ws.uidx[(size_t)b * kUMax + u];
+    }
+    ws.qerr[(size_t)b * kQuantTasks + task] = err;
+    ws.qidx[(size_t)b * kQuantTasks + task] = tidx;
+}
+
 // K1 (integral blocks): register-resident partition quantisation
 template <int DIM>
 __global__ void __launch_bounds__(256, 2) k_quant_reg(Params p, Workspace ws, int task0, int ntasks)
@@ -1786,6 +1858,43 @@ static void build_sp_table(std::vector<SpEntry> &tab)
                         }
 }
 
+// distinct subset problems of modes 0-3 (k_quant_sub): 8-cluster ones first
+static int build_subset_problems(std::vector<uint32_t> &prob, std::vector<uint32_t> &minpart, std::vector<uint16_t> &tsub)
+{
+    prob.clear();
+    minpart.clear();
+    tsub.assign(208 * 3, 0xFFFF);
+    auto mask_of = [](uint32_t shape, int j) {
+        uint32_t m = 0;
+        for (int t = 0; t < 16; ++t) m |= (((shape >> (2 * t)) & 3u) == (uint32_t)j ? 1u : 0u) << t;
+        return m;
+    };
+    for (int pass = 0; pass < 2; ++pass)   // 8 clusters (modes 0, 1), then 4 (modes 2, 3)
+        for (int task = 0; task < 208; ++task) {
+            const int mode = task < 16 ? 0 : task < 80 ? 1 : task < 144 ? 2 : 3;
+            const int part = task < 16 ? task : task < 80 ? task - 16 : task < 144 ? task - 80 : task - 144;
+            const int clog = (mode <= 1) ? 3 : 2;
+            if ((clog == 3) != (pass == 0)) continue;
+            const int subsets = (mode == 0 || mode == 2) ? 3 : 2;
+            const uint32_t shape = subsets == 3 ? kBc7Shape3[part] : kBc7Shape2[part];
+            for (int j = 0; j < subsets; ++j) {
+                const uint32_t key = mask_of(shape, j) | (uint32_t)clog << 16;
+                size_t u = 0;
+                while (u < prob.size() && prob[u] != key) ++u;
+                if (u == prob.size()) {
+                    prob.push_back(key);
+                    minpart.push_back(0xFFFFFFFFu);
+                }
+                const uint32_t cur = (minpart[u] >> (8 * mode)) & 0xFFu;
+                if ((uint32_t)part < cur)
+                    minpart[u] = (minpart[u] & ~(0xFFu << (8 * mode))) | ((uint32_t)part << (8 * mode));
+                tsub[task * 3 + j] = (uint16_t)u;
+            }
+        }
+    return (int)prob.size();
+}
+static int g_nu = 0;
+
 // Per-device state: the single-point table, and two chunk workspaces with two
 // internal streams, so that consecutive chunks run concurrently (one chunk's
 // quantiser beside the other's shakers, and each launch's tail beside the
@@ -1827,6 +1936,14 @@ static hipError_t get_state(uint32_t chunk, int nsets, DeviceState *&out)
         if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dAnchor3a), kBc7Anchor3a, sizeof(kBc7Anchor3a));
         if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dAnchor3b), kBc7Anchor3b, sizeof(kBc7Anchor3b));
         if (e != hipSuccess) return e;
+        std::vector<uint32_t> prob, minpart;
+        std::vector<uint16_t> tsub;
+        g_nu = build_subset_problems(prob, minpart, tsub);
+        if (g_nu > kUMax) return hipErrorInvalidValue;
+        e = hipMemcpyToSymbol(HIP_SYMBOL(dUProb), prob.data(), prob.size() * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dUMinPart), minpart.data(), minpart.size() * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dTaskSub), tsub.data(), tsub.size() * sizeof(uint16_t));
+        if (e != hipSuccess) return e;
         st.device = dev;
     }
     for (int k = 0; k < nsets; ++k) {
@@ -1840,7 +1957,8 @@ static hipError_t get_state(uint32_t chunk, int nsets, DeviceState *&out)
                           align_up(n * kShakeSlots * kShakeRanks * sizeof(ShakeResult)) +
                           align_up(n * kDualTasks * sizeof(DualResult)) + align_up(n * kDualTasks * 2 * sizeof(uint64_t)) +
                           align_up(n * kDualTasks * 2 * sizeof(double)) + align_up(n * sizeof(double)) +
-                          align_up(n * sizeof(uint4));
+                          align_up(n * sizeof(uint4)) + align_up(n * kUMax * sizeof(double)) +
+                          align_up(n * kUMax * sizeof(uint64_t));
         e = hipMalloc(&st.ws_mem[k], sz);
         if (e != hipSuccess) return e;
         Workspace &w = st.ws[k];
@@ -1864,6 +1982,10 @@ static hipError_t get_state(uint32_t chunk, int nsets, DeviceState *&out)
         w.best_err = (double *)p;
         p += align_up(n * sizeof(double));
         w.best_blk = (uint4 *)p;
+        p += align_up(n * sizeof(uint4));
+        w.uerr = (double *)p;
+        p += align_up(n * kUMax * sizeof(double));
+        w.uidx = (uint64_t *)p;
         st.ws_blocks[k] = chunk;
     }
     if (nsets > 1 && !st.lane[0]) {
@@ -1889,8 +2011,11 @@ static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, h
         const uint64_t nq = (uint64_t)p.n * kQuantTasks;
         hipLaunchKernelGGL(k_quant, dim3((uint32_t)((nq + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
         const uint64_t nq3 = (uint64_t)p.n * 208, nq4 = (uint64_t)p.n * 65;
-        if (sm & 0x0Fu)
-            hipLaunchKernelGGL(k_quant_reg<3>, dim3((uint32_t)((nq3 + wg - 1) / wg)), dim3(wg), 0, s, p, ws, 0, 208);
+        if (sm & 0x0Fu) {
+            const uint64_t nu = (uint64_t)p.n * g_nu;
+            hipLaunchKernelGGL(k_quant_sub, dim3((uint32_t)((nu + wg - 1) / wg)), dim3(wg), 0, s, p, ws, g_nu);
+            hipLaunchKernelGGL(k_quant_gather, dim3((uint32_t)((nq3 + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
+        }
         if (sm & 0xC0u)
             hipLaunchKernelGGL(k_quant_reg<4>, dim3((uint32_t)((nq4 + wg - 1) / wg)), dim3(wg), 0, s, p, ws, 208, 65);
         const uint64_t ns = (uint64_t)p.n * kShakeSlots * kShakeRanks;
