@@ -2044,7 +2044,10 @@ static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, h
     }
 }
 
-constexpr uint32_t kChunk = 65536;   // blocks per pipeline pass (~480 MB workspace)
+#ifndef GIC_BC7_CHUNK
+#define GIC_BC7_CHUNK 65536
+#endif
+constexpr uint32_t kChunk = GIC_BC7_CHUNK;   // blocks per pipeline pass (~1.1 GB workspace per set at 65536)
 
 static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t total, const gic_options &o, void *dst,
                              double *err, hipStream_t s)
