@@ -2,12 +2,23 @@
 """Benchmark of the MI355X BCn block-compression hot path.
 
 Metric (BASELINE.json): Mpixels/s (and blocks/s) BC1 & BC7 on 8K RGBA8.
-Default workload = configs[1]: BC1 default quality on an 8192x8192 synthetic
-RGBA8 texture (G1: gradient + noise), inputs resident in HBM, one rank per
-GPU.  With N ranks the job is an (8192*N) x 8192 texture sharded by block
-rows, each rank encoding its own 8192-row shard (weak scaling, no collective
-in the timed region; the optional RCCL gather of the packed bitstream is
-timed separately with --gather).
+
+--workload 8k (default) = configs[1]: BC1 default quality on an 8192x8192
+synthetic RGBA8 texture (G1: gradient + noise), inputs resident in HBM, one
+rank per GPU.  With N ranks the job is an (8192*N) x 8192 texture sharded by
+block rows, each rank encoding its own 8192-row shard (weak scaling, no
+collective in the timed region; the optional RCCL gather of the packed
+bitstream is timed separately with --gather).  The same line carries a
+configs[3] leg (BC7 default quality over the same texture, one pass) and
+configs[2] legs (BC4 R8 height map, BC5 RG8 normal map, 8192^2).
+
+--workload batch64 = configs[4]: BC7 over a fixed 64 x 4096^2 G1 stack, every
+slice's block rows split over the N ranks (strong scaling), one timed RCCL
+all-gather of the packed bitstream at the end.
+
+--gpus N without torchrun's environment starts N ranks itself (a
+torch.distributed.run child process, before any GPU call); under torchrun
+--gpus must equal WORLD_SIZE.
 
 A "step" = one launch of the encoder over the rank's whole shard.  value =
 pixels of all ranks x steps / max-over-ranks wall time.  roofline: the
@@ -55,7 +66,49 @@ def parse():
     p.add_argument("--bc7-rows", type=int, default=-1,
                    help="with the default BC1 workload, also time BC7 on this many block rows of the same "
                         "texture (-1 = the whole 8K texture, 0 = skip)")
+    p.add_argument("--no-bc45", action="store_true", help="skip the BC4/BC5 8K legs (configs[2])")
+    p.add_argument("--workload", default="8k", choices=["8k", "batch64"],
+                   help="8k: configs[1] (+ configs[2]/[3] legs); batch64: configs[4], BC7 over a fixed stack "
+                        "of --batch-slices x --batch-size^2 G1 slices, block rows of every slice split over "
+                        "the ranks (strong scaling) and one timed RCCL gather to rank 0")
+    p.add_argument("--batch-slices", type=int, default=64)
+    p.add_argument("--batch-size", type=int, default=4096)
     return p.parse_args()
+
+
+def cpu_model():
+    """The host CPU model and the threads this process may use (BASELINE.md plan)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model
+
+
+def relaunch_if_needed(args):
+    """--gpus N > 1 without a torchrun environment: start N ranks with
+    torch.distributed.run as a CHILD process (before this process touches the
+    GPU; no exec) and return its exit code.  None = run in this process."""
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None:
+        if args.gpus <= 1:
+            return None
+        import socket
+        import subprocess
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+        return subprocess.call(cmd)
+    if int(world_env) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}; they must agree")
+    return None
 
 
 def make_source(fmt, size, rank, device):
@@ -173,8 +226,7 @@ def bc7_secondary(args, gic, src, size, avail_rows, world, dev, rank):
     if rank == 0 and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-        threads = max(1, min(threads, os.cpu_count() or 1, 64))
+        threads = _cpu_threads()
         host = src.cpu().numpy()[0]
         c0 = time.perf_counter()
         ref = oracle_lib.encode_image_bc7(host, quality=args.bc7_quality, first_row=0, num_rows=1, threads=threads)
@@ -182,14 +234,185 @@ def bc7_secondary(args, gic, src, size, avail_rows, world, dev, rank):
         got = dst.cpu().numpy().reshape(-1, 16)[:bx]
         same = int((got == ref).all(axis=1).sum())
         res["cpu_baseline"] = {"value": round(4 * size / dt / 1e6, 5), "unit": "Mpixels/s", "cores": threads,
-                               "kind": "port", "sample": f"block row 0 ({bx} blocks, {dt:.1f} s, {threads} threads)",
+                               "kind": "port", "cpu_model": cpu_model(), "sample": f"block row 0 ({bx} blocks, {dt:.1f} s, {threads} threads)",
                                "blocks_per_s": round(bx / dt, 1)}
         res["gpu_parity"] = f"{same}/{bx} blocks of the sampled row bit-identical"
     return res
 
 
+def _timed(world, dev, stream, fn, steps):
+    """Barrier + sync on both sides of `steps` calls of fn; returns
+    (max-over-ranks wall s, max-over-ranks event ms per step on `stream`)."""
+    import torch
+    import torch.distributed as dist
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        fn()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    t = _max_over_ranks(torch.tensor([wall, ev0.elapsed_time(ev1) / steps], dtype=torch.float64, device=dev), world)
+    return float(t[0]), float(t[1])
+
+
+def bc45_leg(args, gic, fmt, world, dev, rank):
+    """configs[2]: BC4 on an R8 8192^2 height map (channel 0) or BC5 on its RG8
+    normal map; steps x one launch over the rank's whole texture, plus (rank 0)
+    a bit-exactness check of 16 block rows against the CPU restatement."""
+    import numpy as np
+    import torch
+    size = args.size
+    bx = by = (size + 3) // 4
+    src = make_source(fmt, size, rank, dev)
+    dst = torch.empty(bx * by * gic.block_bytes(fmt), dtype=torch.uint8, device=dev)
+    opts = gic.Options(bc4_channel=0)
+    stream = torch.cuda.current_stream(dev)
+    ch = CHANNELS[fmt]
+
+    def step():
+        gic.encode_device(fmt, src, size, size, 1, ch, dst, opts, 0, by, stream=stream)
+    for _ in range(max(1, args.warmup)):
+        step()
+    wall, kern_ms = _timed(world, dev, stream, step, args.steps)
+    alg = ALG_BYTES[fmt] * bx * by
+    res = {"metric": f"Mpixels/s {'BC4 R8 height' if fmt == 4 else 'BC5 RG8 normal'} {size}x{size}",
+           "value": round(size * size * world * args.steps / wall / 1e6, 3), "unit": "Mpixels/s",
+           "ms_per_step": round(wall / args.steps * 1e3, 4), "kernel_ms": round(kern_ms, 4),
+           "roofline": {"bound": "hbm", "achieved": round(alg / (kern_ms * 1e-3) / 1e9, 3), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(alg / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
+                        "alg_bytes_per_launch": alg}}
+    if rank == 0 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        host = src.cpu().numpy()[0]
+        rows = 16
+        threads = _cpu_threads()
+        c0 = time.perf_counter()
+        ref = oracle_lib.encode_image(fmt, host, bc4_channel=0, first_row=0, num_rows=rows, threads=threads)
+        dt = time.perf_counter() - c0
+        got = dst.cpu().numpy().reshape(-1, gic.block_bytes(fmt))[:rows * bx]
+        res["cpu_baseline"] = {"value": round(rows * 4 * size / dt / 1e6, 4), "unit": "Mpixels/s",
+                               "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+                               "sample": f"block rows 0-{rows - 1} ({rows * bx} blocks, {dt:.2f} s)"}
+        res["gpu_parity"] = "bit-exact" if np.array_equal(got, ref) else \
+            f"{int((got != ref).any(axis=1).sum())} blocks differ"
+    return res
+
+
+def _cpu_threads():
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    return max(1, min(threads, os.cpu_count() or 1, 64))
+
+
+def batch_workload(args, gic, world, rank, dev):
+    """configs[4]: BC7 (quality 1) over a fixed stack of S G1 slices (slice s
+    seeded 0x9E3779B9+s), every slice's block rows split over the ranks
+    (shard.shard_rows, strong scaling: the batch is fixed, each rank does 1/N);
+    a step = one gic_hip_encode_rows call over the rank's rows of all slices.
+    After the timed steps one RCCL all-gather brings every shard to every rank
+    and rank 0 restores the reference block order, timed separately."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from gfx_imagecompress_amd import shard, synth
+    S, n = args.batch_slices, args.batch_size
+    bx = by = (n + 3) // 4
+    first, rows = shard.shard_rows(by, world, rank)
+    src = synth.g1_torch(n, n, S, seed=0x9E3779B9, device=dev)
+    dst = torch.empty(max(1, S * rows * bx * 16), dtype=torch.uint8, device=dev)
+    opts = gic.Options(bc7_quality=args.bc7_quality)
+    stream = torch.cuda.current_stream(dev)
+    # warm-up: the per-device tables and workspaces (one block row of one slice)
+    gic.encode_device(7, src[:1], n, n, 1, 4, dst, opts, first, 1, stream=stream)
+    for _ in range(args.warmup):
+        gic.encode_device(7, src, n, n, S, 4, dst, opts, first, rows, stream=stream)
+
+    def step():
+        gic.encode_device(7, src, n, n, S, 4, dst, opts, first, rows, stream=stream)
+    wall, kern_ms = _timed(world, dev, stream, step, args.steps)
+    gather_ms = None
+    full = dst
+    if world > 1:
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        g0 = time.perf_counter()
+        if dist.get_backend() == "gloo":
+            parts = [torch.empty(shard.shard_rows(by, world, r)[1] * bx * S * 16, dtype=torch.uint8)
+                     for r in range(world)]
+            most = max(p.numel() for p in parts)
+            buf = [torch.empty(most, dtype=torch.uint8) for _ in range(world)]
+            loc = torch.zeros(most, dtype=torch.uint8)
+            loc[:dst.numel()] = dst.cpu()[:S * rows * bx * 16]
+            dist.all_gather(buf, loc)
+            full = shard.assemble([b[:p.numel()] for b, p in zip(buf, parts)], 7, n, n, S)
+        else:
+            full = shard.gather_blocks(dst[:S * rows * bx * 16], 7, n, n, S, world)
+        torch.cuda.synchronize(dev)
+        gather_ms = (time.perf_counter() - g0) * 1e3
+        g = _max_over_ranks(torch.tensor([gather_ms], dtype=torch.float64, device=dev), world)
+        gather_ms = float(g[0])
+    total_blocks = S * bx * by
+    line = None
+    if rank == 0:
+        line = {
+            "metric": "Mpixels/s (and blocks/s) BC1 & BC7 on 8K RGBA8 at 1/2/4/8 MI355X",
+            "value": round(S * n * n * args.steps / wall / 1e6, 4),
+            "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f64+int32", "data": "synthetic",
+            "config": {"workload": f"configs[4]: BC7 quality {args.bc7_quality:g} on a batch of {S}x{n}x{n} "
+                                   f"RGBA8 G1 slices (seed 0x9E3779B9+s), block rows of every slice split over "
+                                   f"{world} rank(s), RCCL all-gather to rank 0 timed separately",
+                       "format": "BC7", "slices": S, "width": n, "global_batch_blocks": total_blocks,
+                       "parallelism": f"block-row shards x{world}",
+                       "world_size_seen": dist.get_world_size() if world > 1 else 1},
+            "blocks_per_s": round(total_blocks * args.steps / wall, 1),
+            "kernel_ms": round(kern_ms, 3),
+            "gather_ms": None if gather_ms is None else round(gather_ms, 3),
+            "roofline": {"bound": "hbm", "achieved": round(80 * S * rows * bx / (kern_ms * 1e-3) / 1e9, 4),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(80 * S * rows * bx / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 8),
+                         "traffic": None, "alg_bytes_per_launch": 80 * S * rows * bx,
+                         "note": "VALU bound; HBM fraction per BASELINE.json"},
+            "cpu_baseline": None,
+        }
+        host_rows = full.cpu().numpy().reshape(S, by, bx, 16) if full.numel() == total_blocks * 16 else None
+        if not args.no_cpu and host_rows is not None:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import oracle_lib
+            threads = _cpu_threads()
+            sl, row = S - 1, by // 2
+            img = synth.g1(n, n, seed=0x9E3779B9 + sl)
+            c0 = time.perf_counter()
+            ref = oracle_lib.encode_image_bc7(img, quality=args.bc7_quality, first_row=row, num_rows=1,
+                                              threads=threads)
+            dt = time.perf_counter() - c0
+            same = int((host_rows[sl, row] == ref).all(axis=1).sum())
+            line["cpu_baseline"] = {"value": round(4 * n / dt / 1e6, 6), "unit": "Mpixels/s", "cores": threads,
+                                    "kind": "port", "cpu_model": cpu_model(),
+                                    "sample": f"slice {sl} block row {row} ({bx} blocks, {dt:.1f} s)",
+                                    "blocks_per_s": round(bx / dt, 1)}
+            line["gpu_parity"] = f"{same}/{bx} blocks of slice {sl} row {row} (after the gather) bit-identical"
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    rc = relaunch_if_needed(args)
+    if rc is not None:
+        sys.exit(rc)
     import torch
     import torch.distributed as dist
     import gfx_imagecompress_amd as gic
@@ -207,7 +430,11 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group("gloo")
+        if dist.get_world_size() != world:
+            raise SystemExit(f"process group has {dist.get_world_size()} ranks, WORLD_SIZE={world}")
     dev = torch.device("cuda", local)
+    if args.workload == "batch64":
+        return batch_workload(args, gic, world, rank, dev)
     fmt = FMTS[args.format]
     size = args.size
     bx, by = (size + 3) // 4, (size + 3) // 4
@@ -224,24 +451,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps
-    t = _max_over_ranks(torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev), world)
-    wall, kern_ms = float(t[0]), float(t[1])
+    wall, kern_ms = _timed(world, dev, stream, step, args.steps)
 
     gather_ms = None
     if args.gather and world > 1:
@@ -290,6 +500,10 @@ def main():
     bc7 = None
     if fmt == 1 and args.bc7_rows != 0:
         bc7 = bc7_secondary(args, gic, src, size, rows, world, dev, rank)
+    bc45 = {}
+    if fmt == 1 and not args.no_bc45:
+        for f in (4, 5):
+            bc45[f"bc{f}"] = bc45_leg(args, gic, f, world, dev, rank)
 
     cpu = None
     parity = None
@@ -298,6 +512,7 @@ def main():
         torch.cuda.synchronize(dev)
         cpu, parity, mism = cpu_baseline(fmt, host, size, dst.cpu().numpy(), args.cpu_seconds, rows, args.bc7_quality)
         cpu["gpu_parity"] = "bit-exact" if parity else f"{mism} blocks differ"
+        cpu["cpu_model"] = cpu_model()
 
     if rank == 0:
         line = {
@@ -317,7 +532,8 @@ def main():
                                    f"{'RGBA8 G1 gradient+noise' if fmt in (1, 7) else ('R8 height' if fmt == 4 else 'RG8 normal')}"
                                    f", block-row shards of {size}x{rows * 4} per GPU",
                        "format": args.format.upper(), "width": size, "rows_per_gpu": rows * 4,
-                       "global_batch_blocks": nblocks * world, "parallelism": f"block-row shards x{world}"},
+                       "global_batch_blocks": nblocks * world, "parallelism": f"block-row shards x{world}",
+                       "world_size_seen": dist.get_world_size() if world > 1 else 1},
             "blocks_per_s": round(nblocks * world * args.steps / wall, 1),
             "kernel_ms": round(kern_ms, 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -333,6 +549,7 @@ def main():
             line["gather_ms"] = round(gather_ms, 3)
         if bc7 is not None:
             line["bc7"] = bc7
+        line.update(bc45)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

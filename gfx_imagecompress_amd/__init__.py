@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, replace
 
 __all__ = [
     "GicError", "Options", "FMT_BC1", "FMT_BC4", "FMT_BC5", "FMT_BC7", "library",
@@ -182,8 +182,29 @@ def encode_device(fmt: int, src, width: int, height: int, slices: int, channels:
 
 
 def encode_blocks_f32(fmt: int, blocks, dst, options: Options | None = None, block_err=None, stream=None) -> None:
-    """Block-level batch: blocks is a float32 CUDA tensor (n,64) for BC1/BC7 or (n,16) for BC4."""
+    """Block-level batch: blocks is a float32 CUDA tensor (n,64) for BC1/BC7 or (n,16) for BC4.
+
+    The batched form of ``Image_CompressAMDBC1Block`` / ``Image_CompressAMDAlphaSingleModeBlock`` /
+    ``Image_CompressAMDMultiModeLDRBlock`` (reference imagecompress.h:117-136).
+    """
+    import torch
+    if fmt not in (FMT_BC1, FMT_BC4, FMT_BC7):
+        raise GicError(f"encode_blocks_f32: format {fmt} has no block-level entry (BC1, BC4, BC7)")
+    if not (blocks.is_cuda and dst.is_cuda):
+        raise GicError("encode_blocks_f32 needs device (HBM) tensors; there is no CPU path")
+    if blocks.dtype != torch.float32 or not blocks.is_contiguous():
+        raise GicError("blocks must be a contiguous float32 tensor")
+    per = 16 if fmt == FMT_BC4 else 64
+    if blocks.dim() != 2 or blocks.shape[1] != per:
+        raise GicError(f"blocks must have shape (n, {per}) for format {fmt}, got {tuple(blocks.shape)}")
     n = blocks.shape[0]
+    if n == 0:
+        return
+    if not dst.is_contiguous() or dst.numel() * dst.element_size() < n * block_bytes(fmt):
+        raise GicError(f"dst too small or not contiguous: need {n * block_bytes(fmt)} bytes")
+    if block_err is not None and (not block_err.is_cuda or block_err.dtype != torch.float64
+                                  or not block_err.is_contiguous() or block_err.numel() < n):
+        raise GicError("block_err must be a contiguous float64 device tensor with one entry per block")
     opts = (options or Options()).to_c()
     rc = library().gic_hip_encode_blocks_f32(fmt, blocks.data_ptr(), n, ctypes.byref(opts), dst.data_ptr(),
                                              block_err.data_ptr() if block_err is not None else None,
@@ -216,7 +237,7 @@ def compress_bc1(image, options: Options | None = None):
     """Image_CompressAMDBC1 (amd_bc1_compressor.cpp:11-71) on a host array."""
     o = options or Options()
     if image.ndim >= 3 and image.shape[-1] < 4:
-        o.force_alpha_one = True
+        o = replace(o, force_alpha_one=True)   # the caller's Options stay untouched
     return _host_compress(FMT_BC1, image, o)
 
 
@@ -234,5 +255,5 @@ def compress_bc7(image, options: Options | None = None):
     """Image_CompressAMDBC7 (amd_bc7_compressor.cpp:25-81)."""
     o = options or Options()
     if image.ndim >= 3 and image.shape[-1] < 4:
-        o.force_alpha_one = True
+        o = replace(o, force_alpha_one=True)
     return _host_compress(FMT_BC7, image, o)

@@ -1915,40 +1915,60 @@ static DeviceState g_states[64];
 
 static size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
 
+// Caller holds g_state_lock.  Tables are published (st.sp set) only after
+// every upload succeeded; a workspace is reallocated only after its lane has
+// drained, since earlier calls may still be using it.
 static hipError_t get_state(uint32_t chunk, int nsets, DeviceState *&out)
 {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-    std::lock_guard<std::mutex> lk(g_state_lock);
     DeviceState &st = g_states[dev];
     if (!st.sp) {
         std::vector<SpEntry> tab;
         build_sp_table(tab);
-        e = hipMalloc(&st.sp, tab.size() * sizeof(SpEntry));
+        SpEntry *sp = nullptr;
+        e = hipMalloc(&sp, tab.size() * sizeof(SpEntry));
         if (e != hipSuccess) return e;
-        e = hipMemcpy(st.sp, tab.data(), tab.size() * sizeof(SpEntry), hipMemcpyHostToDevice);
-        if (e != hipSuccess) return e;
-        e = hipMemcpyToSymbol(HIP_SYMBOL(dShape2), kBc7Shape2, sizeof(kBc7Shape2));
+        e = hipMemcpy(sp, tab.data(), tab.size() * sizeof(SpEntry), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dShape2), kBc7Shape2, sizeof(kBc7Shape2));
         if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dShape3), kBc7Shape3, sizeof(kBc7Shape3));
         if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dAnchor2), kBc7Anchor2, sizeof(kBc7Anchor2));
         if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dAnchor3a), kBc7Anchor3a, sizeof(kBc7Anchor3a));
         if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dAnchor3b), kBc7Anchor3b, sizeof(kBc7Anchor3b));
-        if (e != hipSuccess) return e;
         std::vector<uint32_t> prob, minpart;
         std::vector<uint16_t> tsub;
-        g_nu = build_subset_problems(prob, minpart, tsub);
-        if (g_nu > kUMax) return hipErrorInvalidValue;
-        e = hipMemcpyToSymbol(HIP_SYMBOL(dUProb), prob.data(), prob.size() * sizeof(uint32_t));
-        if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dUMinPart), minpart.data(), minpart.size() * sizeof(uint32_t));
+        const int nu = build_subset_problems(prob, minpart, tsub);
+        if (e == hipSuccess && nu > kUMax) e = hipErrorInvalidValue;
+        if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dUProb), prob.data(), prob.size() * sizeof(uint32_t));
+        if (e == hipSuccess)
+            e = hipMemcpyToSymbol(HIP_SYMBOL(dUMinPart), minpart.data(), minpart.size() * sizeof(uint32_t));
         if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dTaskSub), tsub.data(), tsub.size() * sizeof(uint16_t));
-        if (e != hipSuccess) return e;
+        if (e != hipSuccess) {
+            (void)hipFree(sp);
+            return e;
+        }
+        g_nu = nu;
         st.device = dev;
+        st.sp = sp;
+    }
+    if (!st.lane[0]) {
+        for (int k = 0; k < 2; ++k) {
+            e = hipStreamCreateWithFlags(&st.lane[k], hipStreamNonBlocking);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&st.ev_join[k], hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+        e = hipEventCreateWithFlags(&st.ev_fork, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
     }
     for (int k = 0; k < nsets; ++k) {
         if (st.ws_blocks[k] >= chunk) continue;
-        if (st.ws_mem[k]) (void)hipFree(st.ws_mem[k]);
+        if (st.ws_mem[k]) {
+            e = hipStreamSynchronize(st.lane[k]);   // earlier calls' passes on this workspace
+            if (e != hipSuccess) return e;
+            (void)hipFree(st.ws_mem[k]);
+        }
         st.ws_mem[k] = nullptr;
         st.ws_blocks[k] = 0;
         const size_t n = chunk;
@@ -1987,15 +2007,6 @@ static hipError_t get_state(uint32_t chunk, int nsets, DeviceState *&out)
         p += align_up(n * kUMax * sizeof(double));
         w.uidx = (uint64_t *)p;
         st.ws_blocks[k] = chunk;
-    }
-    if (nsets > 1 && !st.lane[0]) {
-        for (int k = 0; k < 2; ++k) {
-            e = hipStreamCreateWithFlags(&st.lane[k], hipStreamNonBlocking);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&st.ev_join[k], hipEventDisableTiming);
-            if (e != hipSuccess) return e;
-        }
-        e = hipEventCreateWithFlags(&st.ev_fork, hipEventDisableTiming);
-        if (e != hipSuccess) return e;
     }
     out = &st;
     return hipSuccess;
@@ -2053,23 +2064,26 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
                              double *err, hipStream_t s)
 {
     const uint32_t chunk = total < kChunk ? total : kChunk;
-    // GIC_BC7_SINGLE_STREAM=1: every chunk on the caller's stream (per-kernel
-    // profiles then attribute time without the two lanes' overlap)
+    // GIC_BC7_SINGLE_STREAM=1: every chunk on one lane (per-kernel profiles
+    // then attribute time without the two lanes' overlap)
     static const bool single_stream = getenv("GIC_BC7_SINGLE_STREAM") && atoi(getenv("GIC_BC7_SINGLE_STREAM"));
     const int nsets = (total > chunk && !single_stream) ? 2 : 1;
+    // Workspace k is used only on lane k, and a call enqueues all its passes
+    // while holding the device lock: concurrent calls (other threads, other
+    // caller streams) are serialised in lane order, never interleaved on a
+    // workspace.  The caller's stream is joined by fork/join events.
+    std::lock_guard<std::mutex> lk(g_state_lock);
     DeviceState *st = nullptr;
     hipError_t e = get_state(chunk, nsets, st);
     if (e != hipSuccess) return e;
-    if (nsets > 1) {   // fork: both lanes start after the caller's prior work
-        e = hipEventRecord(st->ev_fork, s);
-        for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipStreamWaitEvent(st->lane[k], st->ev_fork, 0);
-        if (e != hipSuccess) return e;
-    }
+    e = hipEventRecord(st->ev_fork, s);   // fork: the lanes start after the caller's prior work
+    for (int k = 0; k < nsets && e == hipSuccess; ++k) e = hipStreamWaitEvent(st->lane[k], st->ev_fork, 0);
+    if (e != hipSuccess) return e;
     const hipStream_t caller = s;
     uint32_t ci = 0;
     for (uint32_t first = 0; first < total; first += chunk, ++ci) {
         const Workspace &ws = st->ws[nsets > 1 ? (ci & 1) : 0];
-        s = nsets > 1 ? st->lane[ci & 1] : caller;
+        s = st->lane[nsets > 1 ? (ci & 1) : 0];
         Params p;
         p.mode_mask = o.bc7_mode_mask;
         p.colour_restrict = o.colour_restrict;
@@ -2118,8 +2132,8 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    if (nsets > 1) {   // join: the caller's stream waits for both lanes
-        for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+    {   // join: the caller's stream waits for the lanes
+        for (int k = 0; k < nsets && e == hipSuccess; ++k) {
             e = hipEventRecord(st->ev_join[k], st->lane[k]);
             if (e == hipSuccess) e = hipStreamWaitEvent(caller, st->ev_join[k], 0);
         }

@@ -134,3 +134,31 @@ def test_two_rank_shards_reassemble_to_single_process_encode():
         # uneven split: 3 + 2 block rows of 9 blocks, 2 slices
         bb = 8 if fmt == 1 else 16
         assert got[0][i][2] == 3 * 9 * 2 * bb and got[1][i][2] == 2 * 9 * 2 * bb
+
+
+def test_bench_gpus_flag_launches_ranks(monkeypatch):
+    """bench.py --gpus N outside torchrun starts N ranks as a child
+    torch.distributed.run (no exec, before any GPU call); under torchrun a
+    WORLD_SIZE that disagrees with --gpus is an error, not a silent N=1 run."""
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    seen = {}
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(subprocess, "call", lambda cmd: seen.setdefault("cmd", cmd) and 0)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "3"])
+    args = bench.parse()
+    assert bench.relaunch_if_needed(args) == 0
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "3"]
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    assert bench.relaunch_if_needed(bench.parse()) is None          # N=1 runs in-process
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    assert bench.relaunch_if_needed(bench.parse()) is None          # torchrun rank
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8"])
+    with pytest.raises(SystemExit):
+        bench.relaunch_if_needed(bench.parse())
