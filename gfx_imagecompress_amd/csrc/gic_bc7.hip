@@ -1520,6 +1520,19 @@ __device__ __forceinline__ int dual_shake_size(const Params &p)
     return (int)(shake > 2 ? shake : 2);
 }
 
+// Index bits of one half (0 = colour, 1 = alpha) of a dual-index candidate:
+// ib0 for the half the selector gives the first index set.  Written as a select
+// on purpose: the round-1 merged dual-quantiser kernel indexed a private copy
+// {ib0, ib1} with this lane-divergent subscript, the optimiser folded it into a
+// load from the __constant__ kModes table and emitted it as a scalar load of
+// the FIRST lane's address (v_readfirstlane + s_load, tools/isa_audit.py), so
+// every lane quantised with lane 0's cluster count (mode 4 mixes 2- and 3-bit
+// sets).  Kernels index no private copies of constant tables by lane values.
+__device__ __forceinline__ int dual_index_bits(const ModeInfo &mi, int half, int sel)
+{
+    return (half ^ sel) ? mi.ib1 : mi.ib0;
+}
+
 __device__ __forceinline__ void dual_task(uint32_t task, int &mode, int &rot, int &sel)
 {
     mode = task < 8 ? 4 : 5;
@@ -1538,7 +1551,7 @@ __global__ void __launch_bounds__(256, 2) k_dual_quant_reg(Params p, Workspace w
     const BlockMeta meta = ws.meta[b];
     if (!mode_active(meta, p, mode) || (meta.flags & 3u) != 2u) return;
     const ModeInfo &mi = kModes[mode];
-    const int ncl = 1 << (half ? (sel ? mi.ib0 : mi.ib1) : (sel ? mi.ib1 : mi.ib0));
+    const int ncl = 1 << dual_index_bits(mi, (int)half, sel);
     const float *tex = ws.tex + (size_t)b * 64;
     const int c0 = kRot[rot][half ? 0 : 1], c1 = kRot[rot][half ? 0 : 2], c2 = kRot[rot][half ? 0 : 3];
     uint32_t px[16];
@@ -1565,9 +1578,8 @@ __global__ void __launch_bounds__(256) k_dual_quant(Params p, Workspace ws)
     const BlockMeta meta = ws.meta[b];
     if (!mode_active(meta, p, mode) || (meta.flags & 3u)) return;
     const ModeInfo &mi = kModes[mode];
-    const int ibs[2] = {mi.ib0, mi.ib1};
     const float *tex = ws.tex + (size_t)b * 64;
-    const int ncl = 1 << ibs[half ? 1 ^ sel : sel];
+    const int ncl = 1 << dual_index_bits(mi, (int)half, sel);
     double blk[16][4];
     for (int i = 0; i < 16; ++i) {
         for (int j = 0; j < 3; ++j) blk[i][j] = (double)tex[i * 4 + kRot[rot][half ? 0 : j + 1]];
@@ -1601,7 +1613,6 @@ __global__ void __launch_bounds__(256, 4) k_dual_wave(Params p, Workspace ws, co
     }
     const int shake = dual_shake_size(p);
     const ModeInfo &mi = kModes[mode];
-    const int ibs[2] = {mi.ib0, mi.ib1};
     const float *tex = ws.tex + (size_t)b * 64;
     unsigned px = 0;
     if (ln < 16)
@@ -1610,7 +1621,7 @@ __global__ void __launch_bounds__(256, 4) k_dual_wave(Params p, Workspace ws, co
     wv::make_texels(T, px, 16, 3);
     const uint64_t qi = ws.dqidx[((size_t)b * kDualTasks + task) * 2 + half];
     int idx = T.live ? (int)((qi >> (4 * ln)) & 15u) : 0;
-    const int ib = half ? ibs[1 ^ sel] : ibs[sel];
+    const int ib = dual_index_bits(mi, (int)half, sel);
     const int last = (1 << ib) - 1;
     const int cb = half ? mi.scalar_bits : mi.vector_bits / 3;
     const int bits[4] = {cb, cb, cb, half ? 6 * cb : 2 * 3 * cb};
@@ -1655,7 +1666,6 @@ __global__ void __launch_bounds__(256) k_dual(Params p, Workspace ws, const SpEn
         return;
     }
     const ModeInfo &mi = kModes[mode];
-    const int ibs[2] = {mi.ib0, mi.ib1};
     const float *tex = ws.tex + (size_t)b * 64;
     double cb[16][4], ab[16][4];
     for (int i = 0; i < 16; ++i) {
@@ -1674,7 +1684,7 @@ __global__ void __launch_bounds__(256) k_dual(Params p, Workspace ws, const SpEn
     const int cbits = mi.vector_bits / 3, abits = mi.scalar_bits;
     const int bits0[4] = {cbits, cbits, cbits, 2 * 3 * cbits};
     const int bits1[4] = {abits, abits, abits, 6 * abits};
-    const int last0 = (1 << ibs[sel]) - 1, last1 = (1 << ibs[1 ^ sel]) - 1;
+    const int last0 = (1 << dual_index_bits(mi, 0, sel)) - 1, last1 = (1 << dual_index_bits(mi, 1, sel)) - 1;
     int epo[2][2][4] = {{{0, 0, 0, 0}, {0, 0, 0, 0}}, {{0, 0, 0, 0}, {0, 0, 0, 0}}};
     const bool corners_too = !(meta.max_range > p.shake_thr);
     if (corners_too) shake_corners<double>(sp, cb, &cb[0][0], 16, idx[0], epo[0], last0, bits0, PAR_CART);   // Q9

@@ -242,3 +242,19 @@ def test_bc7_multi_slice_stack(gpu):
         ref = oracle_lib.encode_image(7, host[k], first_row=first, num_rows=rows)
         check_tolerance(got[k], ref, _src_blocks(host[k], first, rows))
         assert np.array_equal(got[k], ref), (k, _mismatch_report(got[k], ref))
+
+
+@pytest.mark.parametrize("mask", [0x10, 0x30])
+def test_bc7_dual_index_regression_blocks(gpu, mask):
+    """The blocks on which the round-1 merged dual-index quantiser build went
+    wrong (mode 4 mixes 2- and 3-bit index sets; the cluster count was read
+    through a scalar load of lane 0's address): 256 opaque noise
+    blocks and 256 G1 blocks, mode 4 (and 4+5) only, every block vs the oracle."""
+    for img in (synth.noise_rgba(64, 64, seed=6, alpha=False), synth.g1(64, 64),
+                synth.noise_rgba(64, 64, seed=5, alpha=True)):
+        blocks = img.reshape(16, 4, 16, 4, 4).transpose(0, 2, 1, 3, 4).reshape(256, 64).astype(np.float32) \
+            / np.float32(255.0)
+        got = _gpu_blocks_f32(blocks, mask)
+        for i, b in enumerate(blocks):
+            enc, _ = oracle_lib.bc7_block(b, mask)
+            assert got[i].tobytes() == enc, (mask, i)
