@@ -20,12 +20,12 @@ import os
 from dataclasses import dataclass, replace
 
 __all__ = [
-    "GicError", "Options", "FMT_BC1", "FMT_BC4", "FMT_BC5", "FMT_BC7", "library",
-    "block_bytes", "blocks_shape", "encode_device", "encode_blocks_f32", "compress_bc1",
-    "compress_bc4", "compress_bc5", "compress_bc7", "LIB_PATH",
+    "GicError", "Options", "FMT_BC1", "FMT_BC2", "FMT_BC3", "FMT_BC4", "FMT_BC5", "FMT_BC7", "library",
+    "block_bytes", "blocks_shape", "encode_device", "encode_blocks_f32", "compress_bc1", "compress_bc2",
+    "compress_bc3", "compress_bc4", "compress_bc5", "compress_bc7", "LIB_PATH",
 ]
 
-FMT_BC1, FMT_BC4, FMT_BC5, FMT_BC7 = 1, 4, 5, 7
+FMT_BC1, FMT_BC2, FMT_BC3, FMT_BC4, FMT_BC5, FMT_BC7 = 1, 2, 3, 4, 5, 7
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GIC_LIBRARY") or os.path.join(_HERE, "lib", "libgfx_imagecompress_amd.so")
 
@@ -51,6 +51,7 @@ class _COptions(ctypes.Structure):
         ("force_alpha_one", ctypes.c_uint8),
         ("bc7_quality", ctypes.c_float),
         ("bc7_performance", ctypes.c_float),
+        ("bc7_shake_ranks", ctypes.c_uint32),
     ]
 
 
@@ -75,6 +76,7 @@ class Options:
     force_alpha_one: bool = False
     bc7_quality: float = 1.0
     bc7_performance: float = 1.0
+    bc7_shake_ranks: int = 0
 
     def to_c(self) -> _COptions:
         o = _COptions()
@@ -90,6 +92,7 @@ class Options:
         o.force_alpha_one = int(bool(self.force_alpha_one))
         o.bc7_quality = float(self.bc7_quality)
         o.bc7_performance = float(self.bc7_performance)
+        o.bc7_shake_ranks = int(self.bc7_shake_ranks)
         return o
 
 
@@ -182,14 +185,14 @@ def encode_device(fmt: int, src, width: int, height: int, slices: int, channels:
 
 
 def encode_blocks_f32(fmt: int, blocks, dst, options: Options | None = None, block_err=None, stream=None) -> None:
-    """Block-level batch: blocks is a float32 CUDA tensor (n,64) for BC1/BC7 or (n,16) for BC4.
+    """Block-level batch: blocks is a float32 CUDA tensor (n,64) for BC1/BC2/BC3/BC7 or (n,16) for BC4.
 
     The batched form of ``Image_CompressAMDBC1Block`` / ``Image_CompressAMDAlphaSingleModeBlock`` /
     ``Image_CompressAMDMultiModeLDRBlock`` (reference imagecompress.h:117-136).
     """
     import torch
-    if fmt not in (FMT_BC1, FMT_BC4, FMT_BC7):
-        raise GicError(f"encode_blocks_f32: format {fmt} has no block-level entry (BC1, BC4, BC7)")
+    if fmt not in (FMT_BC1, FMT_BC2, FMT_BC3, FMT_BC4, FMT_BC7):
+        raise GicError(f"encode_blocks_f32: format {fmt} has no block-level entry (BC1, BC2, BC3, BC4, BC7)")
     if not (blocks.is_cuda and dst.is_cuda):
         raise GicError("encode_blocks_f32 needs device (HBM) tensors; there is no CPU path")
     if blocks.dtype != torch.float32 or not blocks.is_contiguous():
@@ -239,6 +242,22 @@ def compress_bc1(image, options: Options | None = None):
     if image.ndim >= 3 and image.shape[-1] < 4:
         o = replace(o, force_alpha_one=True)   # the caller's Options stay untouched
     return _host_compress(FMT_BC1, image, o)
+
+
+def compress_bc2(image, options: Options | None = None):
+    """Image_CompressAMDBC2 (amd_bc2_compressor.cpp:11-58): explicit alpha + 4-colour RGB."""
+    o = options or Options()
+    if image.ndim >= 3 and image.shape[-1] < 4:
+        o = replace(o, force_alpha_one=True)
+    return _host_compress(FMT_BC2, image, o)
+
+
+def compress_bc3(image, options: Options | None = None):
+    """Image_CompressAMDBC3 (amd_bc3_compressor.cpp:11-58): interpolated alpha + 4-colour RGB."""
+    o = options or Options()
+    if image.ndim >= 3 and image.shape[-1] < 4:
+        o = replace(o, force_alpha_one=True)
+    return _host_compress(FMT_BC3, image, o)
 
 
 def compress_bc4(image, options: Options | None = None):

@@ -26,6 +26,8 @@
 namespace gic {
 hipError_t launch_bc1_image(const Geometry &g, float thr, int steps, int force_alpha_one, void *dst, hipStream_t s);
 hipError_t launch_bc45_image(const Geometry &g, int fmt, int channel, void *dst, hipStream_t s);
+hipError_t launch_bc23_image(const Geometry &g, int fmt, int steps, int force_alpha_one, void *dst, hipStream_t s);
+hipError_t launch_bc23_blocks(const float *blocks, uint32_t n, int fmt, int steps, void *dst, hipStream_t s);
 hipError_t launch_bc1_blocks(const float *blocks, uint32_t n, float thr, int steps, void *dst, hipStream_t s);
 hipError_t launch_bc4_blocks(const float *blocks, uint32_t n, void *dst, hipStream_t s);
 hipError_t launch_bc7_image(const Geometry &g, const gic_options &o, void *dst, double *err, hipStream_t s);
@@ -72,12 +74,14 @@ static int check_options(gic_format fmt, const gic_options &o)
     if (o.refinement_steps > 8) return GIC_EINVAL;
     if (fmt == GIC_FMT_BC4 && o.bc4_channel > 3) return GIC_EINVAL;
     if (fmt == GIC_FMT_BC7 && o.bc7_performance != 1.0f) return GIC_EUNSUP;   // optQuantTrace_d path not built
+    if (o.bc7_shake_ranks > 8) return GIC_EINVAL;
     return GIC_OK;
 }
 
 static bool valid_fmt(gic_format f)
 {
-    return f == GIC_FMT_BC1 || f == GIC_FMT_BC4 || f == GIC_FMT_BC5 || f == GIC_FMT_BC7;
+    return f == GIC_FMT_BC1 || f == GIC_FMT_BC2 || f == GIC_FMT_BC3 || f == GIC_FMT_BC4 || f == GIC_FMT_BC5 ||
+           f == GIC_FMT_BC7;
 }
 
 extern "C" int gic_hip_encode_rows(gic_format fmt, const uint8_t *d_src, uint32_t width, uint32_t height,
@@ -122,6 +126,10 @@ extern "C" int gic_hip_encode_rows(gic_format fmt, const uint8_t *d_src, uint32_
     case GIC_FMT_BC1:
         e = gic::launch_bc1_image(g, o.bc1_alpha_threshold, o.refinement_steps, o.force_alpha_one, d_dst, s);
         break;
+    case GIC_FMT_BC2:
+    case GIC_FMT_BC3:
+        e = gic::launch_bc23_image(g, (int)fmt, o.refinement_steps, o.force_alpha_one, d_dst, s);
+        break;
     case GIC_FMT_BC4:
     case GIC_FMT_BC5:
         e = gic::launch_bc45_image(g, (int)fmt, o.bc4_channel, d_dst, s);
@@ -147,7 +155,8 @@ extern "C" int gic_hip_encode_blocks_f32(gic_format fmt, const float *d_blocks, 
                                          uint8_t *d_dst, double *d_block_err, void *stream)
 {
     if (!d_blocks || !d_dst || !n) return GIC_EINVAL;
-    if (fmt != GIC_FMT_BC1 && fmt != GIC_FMT_BC4 && fmt != GIC_FMT_BC7) return GIC_EINVAL;
+    if (fmt != GIC_FMT_BC1 && fmt != GIC_FMT_BC2 && fmt != GIC_FMT_BC3 && fmt != GIC_FMT_BC4 && fmt != GIC_FMT_BC7)
+        return GIC_EINVAL;
     gic_options o;
     gic_default_options(&o);
     if (opt) {
@@ -162,6 +171,8 @@ extern "C" int gic_hip_encode_blocks_f32(gic_format fmt, const float *d_blocks, 
         e = gic::launch_bc1_blocks(d_blocks, n, o.bc1_alpha_threshold, o.refinement_steps, d_dst, s);
     else if (fmt == GIC_FMT_BC4)
         e = gic::launch_bc4_blocks(d_blocks, n, d_dst, s);
+    else if (fmt == GIC_FMT_BC2 || fmt == GIC_FMT_BC3)
+        e = gic::launch_bc23_blocks(d_blocks, n, (int)fmt, o.refinement_steps, d_dst, s);
     else
         e = gic::launch_bc7_blocks(d_blocks, n, o, d_dst, d_block_err, s);
     if (e != hipSuccess) return hip_fail(e);
@@ -192,6 +203,10 @@ extern "C" uint32_t TinyImageFormat_ChannelCount(TinyImageFormat f)
     case TinyImageFormat_R32G32B32A32_SFLOAT:
     case TinyImageFormat_DXBC1_RGBA_UNORM:
     case TinyImageFormat_DXBC1_RGBA_SRGB:
+    case TinyImageFormat_DXBC2_UNORM:
+    case TinyImageFormat_DXBC2_SRGB:
+    case TinyImageFormat_DXBC3_UNORM:
+    case TinyImageFormat_DXBC3_SRGB:
     case TinyImageFormat_DXBC7_UNORM:
     case TinyImageFormat_DXBC7_SRGB: return 4;
     default: return 0;
@@ -202,7 +217,7 @@ extern "C" bool TinyImageFormat_IsSRGB(TinyImageFormat f)
 {
     return f == TinyImageFormat_R8G8B8_SRGB || f == TinyImageFormat_R8G8B8A8_SRGB ||
            f == TinyImageFormat_DXBC1_RGB_SRGB || f == TinyImageFormat_DXBC1_RGBA_SRGB ||
-           f == TinyImageFormat_DXBC7_SRGB;
+           f == TinyImageFormat_DXBC2_SRGB || f == TinyImageFormat_DXBC3_SRGB || f == TinyImageFormat_DXBC7_SRGB;
 }
 
 extern "C" bool TinyImageFormat_IsSigned(TinyImageFormat f)
@@ -437,19 +452,44 @@ extern "C" Image_ImageHeader const *Image_CompressAMDBC7(Image_ImageHeader const
     return encode_host_image(src, GIC_FMT_BC7, f, o, cb, user);
 }
 
-// Formats outside this release's hot path (BC2/BC3/BC6H
-// and the bc7enc16 fast path are "next"): exported for link compatibility,
-// they report failure the way the reference reports any failure (NULL).
-extern "C" Image_ImageHeader const *Image_CompressAMDBC2(Image_ImageHeader const *, Image_CompressAMDBackendOptions const *,
-                                                         Image_CompressProgressFunc, void *)
+// BC2 / BC3 (amd_bc2_compressor.cpp:11-58, amd_bc3_compressor.cpp:11-58): sRGB
+// sources give the sRGB destination; the colour half is the 4-colour fit of
+// gic_bcx.hip encode_rgb4 (the reference's CompRGBBlock is undefined behaviour).
+static Image_ImageHeader const *compress_bc23(Image_ImageHeader const *src, gic_format fmt,
+                                              Image_CompressAMDBackendOptions const *amd, Image_CompressProgressFunc cb,
+                                              void *user)
 {
-    return nullptr;
+    if (!src) return nullptr;
+    amd = amd ? amd : &kDefaultAmd;
+    const bool srgb = TinyImageFormat_IsSRGB(src->format);
+    const TinyImageFormat f = fmt == GIC_FMT_BC2 ? (srgb ? TinyImageFormat_DXBC2_SRGB : TinyImageFormat_DXBC2_UNORM)
+                                                 : (srgb ? TinyImageFormat_DXBC3_SRGB : TinyImageFormat_DXBC3_UNORM);
+    gic_options o;
+    gic_default_options(&o);
+    o.b3d_refinement = amd->b3DRefinement;
+    o.adaptive_weights = amd->AdaptiveColourWeights;
+    o.refinement_steps = amd->RefinementSteps;
+    o.force_alpha_one = TinyImageFormat_ChannelCount(src->format) > 3 ? 0 : 1;
+    return encode_host_image(src, fmt, f, o, cb, user);
 }
-extern "C" Image_ImageHeader const *Image_CompressAMDBC3(Image_ImageHeader const *, Image_CompressAMDBackendOptions const *,
-                                                         Image_CompressProgressFunc, void *)
+
+extern "C" Image_ImageHeader const *Image_CompressAMDBC2(Image_ImageHeader const *src,
+                                                         Image_CompressAMDBackendOptions const *amd,
+                                                         Image_CompressProgressFunc cb, void *user)
 {
-    return nullptr;
+    return compress_bc23(src, GIC_FMT_BC2, amd, cb, user);
 }
+
+extern "C" Image_ImageHeader const *Image_CompressAMDBC3(Image_ImageHeader const *src,
+                                                         Image_CompressAMDBackendOptions const *amd,
+                                                         Image_CompressProgressFunc cb, void *user)
+{
+    return compress_bc23(src, GIC_FMT_BC3, amd, cb, user);
+}
+
+// Outside this release: BC6H and the bc7enc16 fast path
+// are exported for link compatibility and fail the way the reference reports
+// any failure (NULL).
 extern "C" Image_ImageHeader const *Image_CompressAMDBC6H(Image_ImageHeader const *, Image_CompressAMDBackendOptions const *,
                                                           Image_CompressProgressFunc, void *)
 {
@@ -568,16 +608,43 @@ extern "C" void Image_CompressAMDMultiModeLDRBlock(float const input[64], uint8_
     encode_one_block(GIC_FMT_BC7, input, 64, o, out, 16);
 }
 
-// BC2/BC3 component blocks and the bc7enc16 block: not in this release.
-extern "C" void Image_CompressAMDRGBSingleModeBlock(float const *, bool, bool, uint8_t, void *out)
+// BC2/BC3 component blocks (amd_bcx_helpers.cpp:107-181): one BC2 block on the
+// GPU built from the component, the requested half returned.
+extern "C" void Image_CompressAMDRGBSingleModeBlock(float const rgb[48], bool adaptive, bool b3d, uint8_t steps,
+                                                    void *out)
 {
-    fprintf(stderr, "gfx_imagecompress_amd: Image_CompressAMDRGBSingleModeBlock is not implemented\n");
-    memset(out, 0, 8);
+    float blk[64];
+    for (int i = 0; i < 16; ++i) {
+        blk[i * 4 + 0] = rgb[i * 3 + 0];
+        blk[i * 4 + 1] = rgb[i * 3 + 1];
+        blk[i * 4 + 2] = rgb[i * 3 + 2];
+        blk[i * 4 + 3] = 1.0f;
+    }
+    gic_options o;
+    gic_default_options(&o);
+    o.adaptive_weights = adaptive;
+    o.b3d_refinement = b3d;
+    o.refinement_steps = steps;
+    uint8_t b[16];
+    if (encode_one_block(GIC_FMT_BC2, blk, 64, o, b, 16))
+        memcpy(out, b + 8, 8);
+    else
+        memset(out, 0, 8);
 }
-extern "C" void Image_CompressAMDExplictAlphaSingleModeBlock(float const *, void *out)
+extern "C" void Image_CompressAMDExplictAlphaSingleModeBlock(float const alpha[16], void *out)
 {
-    fprintf(stderr, "gfx_imagecompress_amd: Image_CompressAMDExplictAlphaSingleModeBlock is not implemented\n");
-    memset(out, 0, 8);
+    float blk[64];
+    for (int i = 0; i < 16; ++i) {
+        blk[i * 4 + 0] = blk[i * 4 + 1] = blk[i * 4 + 2] = 0.f;
+        blk[i * 4 + 3] = alpha[i];
+    }
+    gic_options o;
+    gic_default_options(&o);
+    uint8_t b[16];
+    if (encode_one_block(GIC_FMT_BC2, blk, 64, o, b, 16))
+        memcpy(out, b, 8);
+    else
+        memset(out, 0, 8);
 }
 extern "C" void Image_CompressRichGel999BC7enc16(uint32_t const *, bool, bool, void *out)
 {

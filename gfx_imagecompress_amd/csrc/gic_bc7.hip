@@ -974,6 +974,153 @@ __device__ void pack_dual(int mode, int sel, int rot, int ep[2][2][4], int idx[2
     }
 }
 
+// ----------------------------------------------------------------- decode ---
+
+// Standard BC7 decode of one block to packed RGBA8 words (BPTC format: mode
+// header, partition / rotation / index-selection fields, endpoints channel by
+// channel, p-bits, two index sets with the anchors' top bits implied,
+// interpolation weights round(64 i / (2^bits - 1)), ((64 - w) e0 + w e1 + 32)
+// >> 6).  One lane per block; the mode fields come from selects and every
+// per-texel quantity from register selects, never from an array indexed by a
+// lane value.  Reserved mode (no header bit): transparent black.
+struct Bits128 {
+    uint64_t lo, hi;
+    int pos;
+    __device__ __forceinline__ uint32_t get(int n)
+    {
+        uint64_t v;
+        if (pos >= 64)
+            v = hi >> (pos - 64);
+        else if (pos + n <= 64)
+            v = lo >> pos;
+        else
+            v = (lo >> pos) | (hi << (64 - pos));
+        pos += n;
+        return (uint32_t)v & ((1u << n) - 1u);
+    }
+};
+
+__device__ __forceinline__ int bptc_weight(int i, int bits)
+{
+    const int n1 = (1 << bits) - 1;
+    return (128 * i + n1) / (2 * n1);
+}
+
+__device__ void bc7_decode_block(const uint32_t w[4], uint32_t px[16])
+{
+    Bits128 br{(uint64_t)w[0] | ((uint64_t)w[1] << 32), (uint64_t)w[2] | ((uint64_t)w[3] << 32), 0};
+    const uint32_t lowbyte = w[0] & 0xffu;
+    if (!lowbyte) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) px[i] = 0;
+        return;
+    }
+    const int mode = __builtin_ctz(lowbyte);
+    br.pos = mode + 1;
+    // subsets, partition bits, rotation bits, selection bits, colour bits, alpha
+    // bits, p-bit kind (0 none, 1 per subset, 2 per endpoint), index bits
+    const int ns = mode == 0 || mode == 2 ? 3 : (mode == 1 || mode == 3 || mode == 7 ? 2 : 1);
+    const int pb = mode == 0 ? 4 : (ns > 1 ? 6 : 0);
+    const int rb = mode == 4 || mode == 5 ? 2 : 0;
+    const int sb = mode == 4 ? 1 : 0;
+    const int cb = mode == 0 ? 4 : (mode == 1 ? 6 : (mode == 2 || mode == 4 || mode == 7 ? 5 : 7));
+    const int ab = mode == 4 ? 6 : (mode == 5 ? 8 : (mode == 6 ? 7 : (mode == 7 ? 5 : 0)));
+    const int pk = mode == 1 ? 1 : (mode == 0 || mode == 3 || mode == 6 || mode == 7 ? 2 : 0);
+    const int ib0 = mode == 6 ? 4 : (mode == 0 || mode == 1 ? 3 : 2);
+    const int ib1 = mode == 4 ? 3 : (mode == 5 ? 2 : 0);
+    const int part = (int)br.get(pb);
+    const int rot = (int)br.get(rb);
+    const int sel = (int)br.get(sb);
+    int ep[3][2][4];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+#pragma unroll
+            for (int e = 0; e < 2; ++e)
+                if (q < ns) ep[q][e][c] = (int)br.get(cb);
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+            if (q < ns) ep[q][e][3] = ab ? (int)br.get(ab) : 255;
+    int pbit[3][2] = {{0, 0}, {0, 0}, {0, 0}};
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        if (q >= ns) continue;
+        if (pk == 2) {
+            pbit[q][0] = (int)br.get(1);
+            pbit[q][1] = (int)br.get(1);
+        } else if (pk == 1) {
+            pbit[q][0] = pbit[q][1] = (int)br.get(1);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                if (q >= ns) continue;
+                int bits = c < 3 ? cb : ab;
+                if (!bits) continue;
+                int v = ep[q][e][c];
+                if (pk) {
+                    v = (v << 1) | pbit[q][e];
+                    bits++;
+                }
+                v <<= (8 - bits);
+                ep[q][e][c] = v | (v >> bits);
+            }
+    const uint32_t shape = ns == 1 ? 0u : (ns == 2 ? dShape2[part] : dShape3[part]);
+    const int a1 = ns == 2 ? (int)dAnchor2[part] : (ns == 3 ? (int)dAnchor3a[part] : 0);
+    const int a2 = ns == 3 ? (int)dAnchor3b[part] : 0;
+    uint32_t i0[16], i1[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const bool anchor = i == 0 || (ns > 1 && i == a1) || (ns > 2 && i == a2);
+        i0[i] = br.get(anchor ? ib0 - 1 : ib0);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) i1[i] = ib1 ? br.get(i == 0 ? ib1 - 1 : ib1) : 0u;
+    const int cbits = ib1 && sel ? ib1 : ib0, abits = ib1 ? (sel ? ib0 : ib1) : ib0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int q = (int)((shape >> (2 * i)) & 3u);
+        const int ci = (int)(ib1 && sel ? i1[i] : i0[i]), ai = (int)(ib1 ? (sel ? i0[i] : i1[i]) : i0[i]);
+        const int wc = bptc_weight(ci, cbits), wa = bptc_weight(ai, abits);
+        int v[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int e0 = q == 0 ? ep[0][0][c] : (q == 1 ? ep[1][0][c] : ep[2][0][c]);
+            const int e1 = q == 0 ? ep[0][1][c] : (q == 1 ? ep[1][1][c] : ep[2][1][c]);
+            const int wt = c < 3 ? wc : wa;
+            v[c] = ((64 - wt) * e0 + wt * e1 + 32) >> 6;
+        }
+        int t;
+        if (rot == 1) { t = v[0]; v[0] = v[3]; v[3] = t; }
+        if (rot == 2) { t = v[1]; v[1] = v[3]; v[3] = t; }
+        if (rot == 3) { t = v[2]; v[2] = v[3]; v[3] = t; }
+        px[i] = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16) | ((uint32_t)v[3] << 24);
+    }
+}
+
+// Squared error of a packed block's decode against the block's texels (x255,
+// RGBA), summed texel by texel, channel by channel, in double.
+__device__ double decoded_sse(const uint32_t w[4], const float *tex)
+{
+    uint32_t px[16];
+    bc7_decode_block(w, px);
+    double e = 0.0;
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const double d = (double)((px[i] >> (8 * c)) & 255u) - (double)tex[i * 4 + c];
+            e += d * d;
+        }
+    return e;
+}
+
 // ---------------------------------------------------------------- kernels ---
 
 struct Params {
@@ -985,6 +1132,15 @@ struct Params {
     // computed on the host exactly as the constructor does
     double quality, shake_thr, err_thr, part_search;
     uint32_t stage_mask;   // modes evaluated by this launch sequence (all, or one per stage)
+    // partitions shaken per mode (CompressSingleIndexBlock's `attempts`,
+    // :695-706, optionally capped by gic_options.bc7_shake_ranks), 4 bits per
+    // mode; computed on the host (set_attempts) and read with a shift so that
+    // a lane-varying mode never indexes a table
+    uint32_t att;
+    // pruned search only (bc7_shake_ranks > 0, no error-threshold exits): the
+    // mode whose packed block decodes closest to the texels wins, not the one
+    // with the least search error (DESIGN.md, BC7 pruned search)
+    int decode_select;
 };
 
 // BlockMeta.flags bit 2: the block met the error threshold in an earlier
@@ -1009,11 +1165,30 @@ __device__ __forceinline__ int mode_tries(const Params &p, int mode)
 
 __device__ __forceinline__ int mode_attempts(const Params &p, int mode)
 {
-    const unsigned tries = (unsigned)mode_tries(p, mode);
-    unsigned attempts = (unsigned)floor(8 * p.quality + 0.5);
-    attempts = attempts < tries ? attempts : tries;
-    attempts = attempts > 1 ? attempts : 1;
-    return (int)attempts;
+    return (int)((p.att >> (4 * mode)) & 15u);
+}
+
+// Host: the constructor-derived `attempts` of every mode (:695-706), capped at
+// `cap` (1..8) when the pruned search is selected (0 = the reference's count).
+static uint32_t host_attempts(const Params &p, int cap)
+{
+    static const unsigned nparts_of[8] = {16, 64, 64, 64, 1, 1, 1, 64};
+    uint32_t att = 0;
+    for (int mode = 0; mode < 8; ++mode) {
+        const unsigned nparts = nparts_of[mode];
+        unsigned tries = nparts;
+        if (p.quality < 0.5) {
+            tries = (unsigned)floor((double)(tries * p.part_search) + 0.5);
+            tries = tries < 1 ? 1 : tries;
+            tries = tries > nparts ? nparts : tries;
+        }
+        unsigned attempts = (unsigned)floor(8 * p.quality + 0.5);
+        attempts = attempts < tries ? attempts : tries;
+        attempts = attempts > 1 ? attempts : 1;
+        if (cap > 0 && attempts > (unsigned)cap) attempts = (unsigned)cap;
+        att |= attempts << (4 * mode);
+    }
+    return att;
 }
 
 __device__ void prep_block(const float inN[64], const Params &p, float *tex, BlockMeta &meta)
@@ -1353,21 +1528,32 @@ __global__ void __launch_bounds__(256) k_shake(Params p, Workspace ws, const SpE
 //   NC = 8 : modes 0, 1 (slots 0, 1)      -> 8 ranks x (3 + 2) subsets = 40
 //   NC = 4 : modes 2, 3, 7 (slots 2, 3, 5) -> 8 x (3 + 2 + 2)          = 56
 //   NC = 16: mode 6 (slot 4)               -> 1
-template <int NC> struct WaveSet;
-template <> struct WaveSet<8> { static constexpr int count = 40; };
-template <> struct WaveSet<4> { static constexpr int count = 56; };
-template <> struct WaveSet<16> { static constexpr int count = 1; };
+// Waves per block of k_shake_wave<NC>: (rank, subset) problems of the slots
+// it serves -- modes 0/1 (NC 8), 2/3/7 (NC 4), 6 (NC 16) -- for the ranks
+// actually shaken (Params.att), rank-major within a slot.
+template <int NC>
+__host__ __device__ static int wave_count(uint32_t att)
+{
+    const int m8[2] = {0, 1}, m4[3] = {2, 3, 7};
+    const int *ms = NC == 8 ? m8 : m4;
+    const int nm = NC == 8 ? 2 : 3;
+    if (NC == 16) return (int)((att >> 24) & 15u) ? 1 : 0;
+    int c = 0;
+    for (int k = 0; k < nm; ++k) c += (int)((att >> (4 * ms[k])) & 15u) * (ms[k] == 0 || ms[k] == 2 ? 3 : 2);
+    return c;
+}
 
 template <int NC>
-__device__ __forceinline__ void wave_problem(int id, int &slot, int &rank, int &subset)
+__device__ __forceinline__ void wave_problem(const Params &p, int id, int &slot, int &rank, int &subset)
 {
     const int nsl = NC == 8 ? 2 : (NC == 4 ? 3 : 1);
-    const int slots8[2] = {0, 1}, slots4[3] = {2, 3, 5};
     int base = 0;
     for (int k = 0; k < nsl; ++k) {
-        const int sl = NC == 8 ? slots8[k] : (NC == 4 ? slots4[k] : 4);
-        const int ns = kModes[kSlotMode[sl]].subsets;
-        const int cnt = (sl == 4 ? 1 : 8) * ns;
+        // slot k of this kernel: 0/1 (NC 8), 2/3/5 (NC 4), 4 (NC 16)
+        const int sl = NC == 8 ? k : (NC == 4 ? (k == 2 ? 5 : 2 + k) : 4);
+        const int md = NC == 8 ? k : (NC == 4 ? (k == 2 ? 7 : 2 + k) : 6);
+        const int ns = NC == 8 ? (k == 0 ? 3 : 2) : (NC == 4 ? (k == 0 ? 3 : 2) : 1);
+        const int cnt = (sl == 4 ? 1 : mode_attempts(p, md)) * ns;
         if (id < base + cnt || k == nsl - 1) {
             slot = sl;
             rank = (id - base) / ns;
@@ -1396,10 +1582,11 @@ template <int NC>
 __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, const SpEntry *__restrict__ sp)
 {
     const uint32_t wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint32_t b = wid / WaveSet<NC>::count;
+    const uint32_t per = (uint32_t)wave_count<NC>(p.att);
+    const uint32_t b = wid / per;
     if (b >= p.n) return;
     int slot, rank, subset;
-    wave_problem<NC>((int)(wid % WaveSet<NC>::count), slot, rank, subset);
+    wave_problem<NC>(p, (int)(wid % per), slot, rank, subset);
     const int mode = kSlotMode[slot];
     const BlockMeta meta = ws.meta[b];
     if (!mode_active(meta, p, mode) || (meta.flags & 3u) != 2u) return;
@@ -1723,7 +1910,8 @@ __global__ void __launch_bounds__(256) k_select(Params p, Workspace ws, uint4 *_
         return;
     }
     const int order[8] = {6, 4, 3, 1, 2, 0, 7, 5};
-    double best = 1.7976931348623157e308;
+    double best = 1.7976931348623157e308, best_d = 1.7976931348623157e308;
+    const float *tex = ws.tex + (size_t)b * 64;
     uint32_t bw[4] = {0, 0, 0, 0};
     if (resume) {
         best = ws.best_err[b];
@@ -1796,7 +1984,14 @@ __global__ void __launch_bounds__(256) k_select(Params p, Workspace ws, uint4 *_
             }
             pack_single(m, (int)shk[bi].part, ep, tidx, w);
         }
-        if (e < best) {
+        if (p.decode_select) {
+            const double d = decoded_sse(w, tex);
+            if (d < best_d) {
+                best_d = d;
+                best = e;
+                for (int q = 0; q < 4; ++q) bw[q] = w[q];
+            }
+        } else if (e < best) {
             best = e;
             for (int q = 0; q < 4; ++q) bw[q] = w[q];
         }
@@ -2041,16 +2236,16 @@ static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, h
             hipLaunchKernelGGL(k_quant_reg<4>, dim3((uint32_t)((nq4 + wg - 1) / wg)), dim3(wg), 0, s, p, ws, 208, 65);
         const uint64_t ns = (uint64_t)p.n * kShakeSlots * kShakeRanks;
         hipLaunchKernelGGL(k_shake, dim3((uint32_t)((ns + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
-        if (sm & 0x03u) {
-            const uint64_t nw8 = (uint64_t)p.n * WaveSet<8>::count * 64;
+        if ((sm & 0x03u) && wave_count<8>(p.att)) {
+            const uint64_t nw8 = (uint64_t)p.n * wave_count<8>(p.att) * 64;
             hipLaunchKernelGGL(k_shake_wave<8>, dim3((uint32_t)((nw8 + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
         }
-        if (sm & 0x8Cu) {
-            const uint64_t nw4 = (uint64_t)p.n * WaveSet<4>::count * 64;
+        if ((sm & 0x8Cu) && wave_count<4>(p.att)) {
+            const uint64_t nw4 = (uint64_t)p.n * wave_count<4>(p.att) * 64;
             hipLaunchKernelGGL(k_shake_wave<4>, dim3((uint32_t)((nw4 + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
         }
         if (sm & 0x40u) {
-            const uint64_t nw16 = (uint64_t)p.n * WaveSet<16>::count * 64;
+            const uint64_t nw16 = (uint64_t)p.n * wave_count<16>(p.att) * 64;
             hipLaunchKernelGGL(k_shake_wave<16>, dim3((uint32_t)((nw16 + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
         }
     }
@@ -2117,6 +2312,8 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
             p.err_thr = 0;
             p.part_search = 1.0;
         }
+        p.att = host_attempts(p, o.bc7_shake_ranks);
+        p.decode_select = o.bc7_shake_ranks > 0 && !(p.err_thr > 0);
         const uint32_t wg = 256;
         if (g)
             hipLaunchKernelGGL(k_prep_image, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, *g, p, ws);

@@ -757,6 +757,73 @@ __device__ __forceinline__ uint2 encode_bc1_f32(const float in[64], int steps, f
     return encode_bc1(u, kept, t, steps, use_alpha);
 }
 
+// --------------------------------------------------------- BC2 / BC3 ---
+
+// Image_CompressAMDRGBSingleModeBlock (amd_bcx_helpers.cpp:142-181), the colour
+// half of BC2 and BC3.  The reference's CompRGBBlock (amd_bcx_body.cpp:1299-1365)
+// is undefined behaviour: its final clustering reads the 48-float RGB input with
+// a stride of 4 (to index 62) and writes a 48-float buffer the same way, and it
+// fits endpoints in R,G,B order but clusters in B,G,R order -- its output depends
+// on stack contents.  This is its well-defined intent, the
+// reference's own 4-colour CompRGBABlock fit with alpha ignored (the BC1 path's
+// second candidate, amd_bcx_helpers.cpp:77-88), packed with c0 > c1 as
+// :164-171 (BC2/BC3 colour blocks are always 4-colour).
+template <class Col, class Tex>
+__device__ __forceinline__ uint2 encode_rgb4(const Col &u, int kept, const Tex &t, int steps)
+{
+    uint8_t ep[3][2];
+    uint32_t ib = 0;
+    comp_rgba<4>(t, steps, false, ep, ib, u, kept);
+    const unsigned c0 = ((unsigned)(ep[CH_R][0] >> 3) << 11) | ((unsigned)(ep[CH_G][0] >> 2) << 5) |
+                        (unsigned)(ep[CH_B][0] >> 3);
+    const unsigned c1 = ((unsigned)(ep[CH_R][1] >> 3) << 11) | ((unsigned)(ep[CH_G][1] >> 2) << 5) |
+                        (unsigned)(ep[CH_B][1] >> 3);
+    uint2 out;
+    out.x = c0 <= c1 ? (c1 | (c0 << 16)) : (c0 | (c1 << 16));
+    out.y = ib;
+    return out;
+}
+
+// Image_CompressAMDExplictAlphaSingleModeBlock (amd_bcx_helpers.cpp:107-123): a
+// = (uint8_t)(alpha * 255.0f), 4 bits per texel rounded as the reference does.
+// For a byte source alpha * 255.0f == the byte; float inputs are clamped to
+// [0, 255] before the conversion (out-of-range is undefined in the reference).
+__device__ __forceinline__ uint32_t explicit_alpha4(uint32_t a)
+{
+    a = (a + ((a >> 4) < 0x8 ? 7u : 8u) - (a >> 4)) >> 4;
+    return a > 0xfu ? 0xfu : a;
+}
+
+__device__ __forceinline__ uint2 encode_explicit_alpha_u8(const uint32_t px[16])
+{
+    uint2 out{0u, 0u};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t a = explicit_alpha4(px[i] >> 24);
+        if (i < 8)
+            out.x |= a << (4 * i);
+        else
+            out.y |= a << (4 * (i - 8));
+    }
+    return out;
+}
+
+__device__ __forceinline__ uint2 encode_explicit_alpha_f32(const float v[16])
+{
+    uint2 out{0u, 0u};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        float f = v[i] * 255.0f;
+        f = f < 0.f ? 0.f : (f > 255.f ? 255.f : f);
+        const uint32_t a = explicit_alpha4((uint32_t)f);
+        if (i < 8)
+            out.x |= a << (4 * i);
+        else
+            out.y |= a << (4 * (i - 8));
+    }
+    return out;
+}
+
 // ------------------------------------------------------------- BC4 ---
 
 // RmpSrch1 evaluated in full, amd_bcx_body.cpp:1510-1548
@@ -993,6 +1060,41 @@ __global__ void __launch_bounds__(256, 2) bc1_image_kernel(Geometry g, Bc1Params
     dst[id] = bcx::encode_bc1_u8(px, p.steps, p.alpha_threshold > 0.0f, p.thr_keep, p.thr_final, lut);
 }
 
+// BC2 / BC3 (amd_bc2_compressor.cpp:36-50, amd_bc3_compressor.cpp:36-50): alpha
+// half (explicit 4-bit, or the BC4 interpolated alpha of
+// Image_CompressAMDAlphaSingleModeBlock) then the 4-colour RGB half, one lane
+// per block.  Alpha is the source's (1.0 without an alpha channel, as
+// ReadNxNSplitBlockF's forceAlphaTo1).
+__global__ void __launch_bounds__(256, 2) bc23_image_kernel(Geometry g, int fmt, Bc1Params p, uint4 *__restrict__ dst)
+{
+    __shared__ float lut[256];   // byte -> v / 255.0f
+    lut[threadIdx.x] = (float)threadIdx.x / 255.0f;
+    __syncthreads();
+    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= g.total) return;
+    uint32_t slice, by, bx;
+    block_coords(g, id, slice, by, bx);
+    uint32_t px[16];
+    load_block_u8(g, slice, by, bx, p.force_alpha_one != 0, px);
+    uint2 a;
+    if (fmt == 3) {
+        float v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = lut[px[i] >> 24];
+        const uint64_t r = bcx::encode_bc4(v);
+        a = make_uint2((uint32_t)r, (uint32_t)(r >> 32));
+    } else {
+        a = bcx::encode_explicit_alpha_u8(px);
+    }
+    bcx::ColB u;
+    u.lut = lut;
+    int kept;
+    bcx::unique_colours(u, px, false, 0u, kept);
+    const bcx::TexB t{px, 0u};
+    const uint2 c = bcx::encode_rgb4(u, kept, t, p.steps);
+    dst[id] = make_uint4(a.x, a.y, c.x, c.y);
+}
+
 __global__ void __launch_bounds__(256) bc45_image_kernel(Geometry g, int fmt, int channel,
                                                          uint64_t *__restrict__ dst)
 {
@@ -1040,6 +1142,31 @@ __global__ void __launch_bounds__(256) bc4_blocks_kernel(const float *__restrict
     dst[id] = bcx::encode_bc4(v);
 }
 
+__global__ void __launch_bounds__(256) bc23_blocks_kernel(const float *__restrict__ blocks, uint32_t n, int fmt,
+                                                          Bc1Params p, uint4 *__restrict__ dst)
+{
+    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= n) return;
+    float blk[64], v[16];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) blk[i] = blocks[(size_t)id * 64 + i];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = blk[i * 4 + 3];
+    uint2 a;
+    if (fmt == 3) {
+        const uint64_t r = bcx::encode_bc4(v);
+        a = make_uint2((uint32_t)r, (uint32_t)(r >> 32));
+    } else {
+        a = bcx::encode_explicit_alpha_f32(v);
+    }
+    bcx::ColF u;
+    int kept;
+    bcx::unique_colours(u, blk, false, 0.f, kept);
+    const bcx::TexF t{blk, 0.f};
+    const uint2 c = bcx::encode_rgb4(u, kept, t, p.steps);
+    dst[id] = make_uint4(a.x, a.y, c.x, c.y);
+}
+
 // ------------------------------------------------------------ launchers ---
 
 // smallest alpha byte passing `pass(a)` (256 if none); pass is monotone in a
@@ -1064,6 +1191,22 @@ hipError_t launch_bc1_image(const Geometry &g, float thr, int steps, int force_a
     const Bc1Params p{thr, steps, force_alpha_one, keep, fin};
     const uint32_t wg = 256, grid = (g.total + wg - 1) / wg;
     hipLaunchKernelGGL(bc1_image_kernel, dim3(grid), dim3(wg), 0, s, g, p, (uint2 *)dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_bc23_image(const Geometry &g, int fmt, int steps, int force_alpha_one, void *dst, hipStream_t s)
+{
+    const Bc1Params p{0.f, steps, force_alpha_one, 0u, 0u};
+    const uint32_t wg = 256, grid = (g.total + wg - 1) / wg;
+    hipLaunchKernelGGL(bc23_image_kernel, dim3(grid), dim3(wg), 0, s, g, fmt, p, (uint4 *)dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_bc23_blocks(const float *blocks, uint32_t n, int fmt, int steps, void *dst, hipStream_t s)
+{
+    const Bc1Params p{0.f, steps, 0, 0u, 0u};
+    const uint32_t wg = 256, grid = (n + wg - 1) / wg;
+    hipLaunchKernelGGL(bc23_blocks_kernel, dim3(grid), dim3(wg), 0, s, blocks, n, fmt, p, (uint4 *)dst);
     return hipGetLastError();
 }
 

@@ -45,6 +45,10 @@ typedef enum TinyImageFormat {
     TinyImageFormat_DXBC5_SNORM,
     TinyImageFormat_DXBC7_UNORM,
     TinyImageFormat_DXBC7_SRGB,
+    TinyImageFormat_DXBC2_UNORM,
+    TinyImageFormat_DXBC2_SRGB,
+    TinyImageFormat_DXBC3_UNORM,
+    TinyImageFormat_DXBC3_SRGB,
     TinyImageFormat_Count
 } TinyImageFormat;
 

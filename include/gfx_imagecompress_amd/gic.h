@@ -29,6 +29,8 @@ extern "C" {
 
 typedef enum gic_format {
     GIC_FMT_BC1 = 1, /* Image_CompressAMDBC1Block semantics (amd_bcx_helpers.cpp:51) */
+    GIC_FMT_BC2 = 2, /* explicit 4-bit alpha (amd_bcx_helpers.cpp:107) + 4-colour RGB half */
+    GIC_FMT_BC3 = 3, /* BC4-style alpha (:125) + 4-colour RGB half (amd_bc3_compressor.cpp:41-46) */
     GIC_FMT_BC4 = 4, /* Image_CompressAMDAlphaSingleModeBlock on one channel (:125) */
     GIC_FMT_BC5 = 5, /* two BC4 blocks, channel 0 then channel 1 (amd_bc5_compressor.cpp:35-41) */
     GIC_FMT_BC7 = 7  /* BC7BlockEncoder::CompressBlock (amd_bc7_body.cpp:1289) */
@@ -50,6 +52,9 @@ typedef struct gic_options {
     uint8_t force_alpha_one;     /* 1: ignore source alpha (ReadNxNBlockF forceAlphaTo1) */
     float bc7_quality;           /* BC7BlockEncoder quality, clamped to [0,1] (default 1.0) */
     float bc7_performance;       /* must be 1.0 in this release */
+    uint32_t bc7_shake_ranks;    /* partitions shaken per single-index BC7 mode: 0 = the reference's
+                                    count (8 at quality 1, bit-exact search); 1..8 caps it (pruned
+                                    search, held to the per-block MSE tolerance) */
 } gic_options;
 
 void gic_default_options(gic_options *opt);

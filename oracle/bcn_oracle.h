@@ -30,6 +30,11 @@ void orc_bc1_block(const float in[64], int refinement_steps,
 /* Image_CompressAMDAlphaSingleModeBlock (amd_bcx_helpers.cpp:125-140). */
 void orc_bc4_block(const float in[16], uint8_t out[8]);
 
+/* BC2/BC3 halves: the 4-colour RGB block (alpha ignored; the reference's
+ * CompRGBBlock is UB, see orc_bcx.c) and the explicit 4-bit alpha block. */
+void orc_rgb4_block(const float in[64], int refinement_steps, uint8_t out[8]);
+void orc_explicit_alpha_block(const float in[16], uint8_t out[8]);
+
 /* BC7BlockEncoder::CompressBlock (amd_bc7_body.cpp:1289-1465) with the
  * encoder constructed as in Image_CompressAMDMultiModeLDRBlock
  * (amd_bc7_compressor.cpp:11-23).  Returns the encoder's block error. */
@@ -37,11 +42,17 @@ double orc_bc7_block(const float in[64], uint8_t mode_mask, int src_has_alpha,
                      float quality, int colour_restrict, int alpha_restrict,
                      float performance, uint8_t out[16]);
 
+/* orc_bc7_block with the GPU's optional shake-rank cap (gic_options.bc7_shake_ranks;
+ * 0 = the reference). */
+double orc_bc7_block_ex(const float in[64], uint8_t mode_mask, int src_has_alpha,
+                        float quality, int colour_restrict, int alpha_restrict,
+                        float performance, int shake_ranks, uint8_t out[16]);
+
 /* Image-level drivers over an 8-bit source (the reference's block loops in
  * amd_bc{1,4,5,7}_compressor.cpp with ReadNxNBlockF edge clamping,
  * block_utils.cpp:7-41, and UNORM8 -> float as v/255.0f).
  * src: rows of width*channels bytes, slices stacked; dst: row-major blocks.
- * fmt: 1 = BC1, 4 = BC4, 5 = BC5, 7 = BC7.  channels in {1,2,3,4}.
+ * fmt: 1 = BC1, 2 = BC2, 3 = BC3, 4 = BC4, 5 = BC5, 7 = BC7.  channels in {1,2,3,4}.
  * bc4_channel selects the source channel for BC4 (reference uses 1).
  * first_row/num_rows restrict to a block-row range (per slice); rows <0 = all.
  * threads: 0/1 = calling thread, N = a pool of N pthreads over block rows. */
@@ -56,6 +67,9 @@ int orc_encode_image(int fmt, const uint8_t *src, uint32_t width, uint32_t heigh
 int orc_encode_image_bc7(const uint8_t *src, uint32_t width, uint32_t height, uint32_t slices, uint32_t channels,
                          int32_t first_row, int32_t num_rows, int threads, float quality, uint8_t mode_mask,
                          uint8_t *dst, double *block_err);
+int orc_encode_image_bc7_ex(const uint8_t *src, uint32_t width, uint32_t height, uint32_t slices, uint32_t channels,
+                            int32_t first_row, int32_t num_rows, int threads, float quality, uint8_t mode_mask,
+                            int shake_ranks, uint8_t *dst, double *block_err);
 
 /* helpers exposed for unit tests */
 void orc_load_block_rgba8(const uint8_t *src, uint32_t width, uint32_t height,

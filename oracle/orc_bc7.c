@@ -928,6 +928,7 @@ typedef struct {
     double stored_err[64];
     int sorted[64];
     int unsupported;
+    int rank_cap;   /* gic_options.bc7_shake_ranks: 0 = reference attempts, 1..8 = cap (pruned GPU search model) */
 } bc7_enc;
 
 static void put_bits(uint8_t *blk, int *pos, unsigned v, int n)
@@ -1102,6 +1103,10 @@ static double single_index(bc7_enc *e, double in[16][4], uint8_t out[16], int mo
     unsigned attempts = (unsigned)floor(8 * e->quality + 0.5);
     attempts = attempts < tries ? attempts : tries;
     attempts = attempts > 1 ? attempts : 1;
+    /* not in the reference: the GPU's optional pruned search shakes only the
+     * first rank_cap partitions (tests compare it with the exact search under
+     * the per-block MSE tolerance) */
+    if (e->rank_cap > 0 && attempts > (unsigned)e->rank_cap) attempts = (unsigned)e->rank_cap;
     if (e->parity == PAR_SAME || e->parity == PAR_BCC) shake += 2;
 
     int epo_code[3][2][4], best_ep[3][2][4], best_idx[3][16], best_cnt[3] = {0, 0, 0};
@@ -1141,6 +1146,7 @@ static double single_index(bc7_enc *e, double in[16][4], uint8_t out[16], int mo
             }
         }
         TRACE(0, mode, (int)i, part, err, sub_err);
+        TRACE(2, mode, (int)i, part, e->stored_err[part], (const double *)0);
         if (err < best_err) {
             best_part = (unsigned)part;
             for (int s = 0; s < mi->subsets; ++s) {
@@ -1284,6 +1290,14 @@ static double dual_index(bc7_enc *e, double in[16][4], uint8_t out[16], int mode
 double orc_bc7_block(const float inN[64], uint8_t mode_mask, int src_has_alpha, float quality_f,
                      int colour_restrict, int alpha_restrict, float performance_f, uint8_t out[16])
 {
+    return orc_bc7_block_ex(inN, mode_mask, src_has_alpha, quality_f, colour_restrict, alpha_restrict, performance_f,
+                            0, out);
+}
+
+double orc_bc7_block_ex(const float inN[64], uint8_t mode_mask, int src_has_alpha, float quality_f,
+                        int colour_restrict, int alpha_restrict, float performance_f, int shake_ranks,
+                        uint8_t out[16])
+{
     (void)src_has_alpha; /* m_imageNeedsAlpha is never read by CompressBlock */
     pthread_once(&g_once, build_tables);
     static __thread bc7_enc enc;
@@ -1296,6 +1310,7 @@ double orc_bc7_block(const float inN[64], uint8_t mode_mask, int src_has_alpha, 
     e->performance = pf < 1.0 ? (pf > 0.0 ? pf : 0.0) : 1.0;
     e->colour_restrict = colour_restrict;
     e->alpha_restrict = alpha_restrict;
+    e->rank_cap = shake_ranks;
     e->quant_thr = 255 * e->performance;
     if (e->quality < 0.5) {
         e->shake_thr = 0.;
@@ -1341,7 +1356,10 @@ double orc_bc7_block(const float inN[64], uint8_t mode_mask, int src_has_alpha, 
     }
     static const int order[8] = {6, 4, 3, 1, 2, 0, 7, 5};
     uint8_t tmp[16];
-    double best = DBL_MAX;
+    double best = DBL_MAX, best_d = DBL_MAX;
+    /* not in the reference: the GPU's pruned search picks the mode whose packed
+     * block decodes closest to the texels (see gic_bc7.hip k_select) */
+    const int decode_select = e->rank_cap > 0 && !(e->err_thr > 0);
     memset(tmp, 0, sizeof(tmp));
     for (int k = 0; k < 8; ++k) {
         const int m = order[k];
@@ -1350,7 +1368,21 @@ double orc_bc7_block(const float inN[64], uint8_t mode_mask, int src_has_alpha, 
         double err = kModes[m].enc != ENC_SEPARATE ? single_index(e, in, tmp, m) : dual_index(e, in, tmp, m);
         if (e->unsupported) return -1.0;
         TRACE(1, m, -1, -1, err, (const double *)0);
-        if (err < best) {
+        if (decode_select) {
+            uint8_t dec[64];
+            double d = 0.0;
+            orc_bc7_decode(tmp, dec);
+            for (int i = 0; i < 16; ++i)
+                for (int c = 0; c < 4; ++c) {
+                    const double t = (double)dec[i * 4 + c] - in[i][c];
+                    d += t * t;
+                }
+            if (d < best_d) {
+                memcpy(out, tmp, 16);
+                best_d = d;
+                best = err;
+            }
+        } else if (err < best) {
             memcpy(out, tmp, 16);
             best = err;
         }

@@ -592,6 +592,46 @@ void orc_bc1_block(const float in[64], int refinement_steps, float alpha_thresho
     memcpy(out8 + 4, &w1, 4);
 }
 
+/* Colour half of BC2/BC3: Image_CompressAMDRGBSingleModeBlock
+ * (amd_bcx_helpers.cpp:142-181).  The reference's CompRGBBlock
+ * (amd_bcx_body.cpp:1299-1365) is undefined behaviour (stride-4 reads past its
+ * 48-float input, endpoints fitted in R,G,B but clustered in B,G,R order), so
+ * this restates its intent -- CompRGBABlock's 4-colour fit with alpha ignored
+ * -- packed with c0 > c1 as :164-171.  Parity of this half is unpinned (no
+ * reference output exists to pin it); the alpha halves are pinned by the BC4
+ * restatement they share. */
+void orc_rgb4_block(const float in[64], int refinement_steps, uint8_t out8[8])
+{
+    const float w[3] = {0.3086f, 0.6094f, 0.0820f};
+    uint8_t ep[3][2], idx[16];
+    comp_rgba_block(in, ep, idx, 4, refinement_steps, w, 0, 0.f);
+    unsigned c0 = ((unsigned)(ep[CH_R][0] >> 3) << 11) | ((unsigned)(ep[CH_G][0] >> 2) << 5) |
+                  (unsigned)(ep[CH_B][0] >> 3);
+    unsigned c1 = ((unsigned)(ep[CH_R][1] >> 3) << 11) | ((unsigned)(ep[CH_G][1] >> 2) << 5) |
+                  (unsigned)(ep[CH_B][1] >> 3);
+    uint32_t w0 = c0 <= c1 ? (c1 | (c0 << 16)) : (c0 | (c1 << 16)), w1 = 0;
+    for (int i = 0; i < 16; ++i)
+        w1 |= (uint32_t)((uint64_t)idx[i] << (2 * i));
+    memcpy(out8, &w0, 4);
+    memcpy(out8 + 4, &w1, 4);
+}
+
+/* Image_CompressAMDExplictAlphaSingleModeBlock, amd_bcx_helpers.cpp:107-123
+ * (float -> byte clamped to [0,255] first: out-of-range is UB there). */
+void orc_explicit_alpha_block(const float in[16], uint8_t out8[8])
+{
+    uint32_t w[2] = {0, 0};
+    for (int i = 0; i < 16; ++i) {
+        float f = in[i] * 255.0f;
+        f = f < 0.f ? 0.f : (f > 255.f ? 255.f : f);
+        unsigned a = (unsigned)(uint8_t)f;
+        a = (a + ((a >> 4) < 0x8 ? 7 : 8) - (a >> 4)) >> 4;
+        if (a > 0xf) a = 0xf;
+        w[i < 8 ? 0 : 1] |= a << ((i % 8) * 4);
+    }
+    memcpy(out8, w, 8);
+}
+
 /* ------------------------------------------------------ scalar (BC4) --- */
 
 /* RmpSrch1, amd_bcx_body.cpp:1510-1548. */

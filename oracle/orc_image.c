@@ -58,6 +58,7 @@ typedef struct {
     double *err;
     float bc7_quality;   /* BC7BlockEncoder quality (image API: 1.0) */
     uint8_t bc7_mask;    /* BC7 ModeMask (image API default 0xFF) */
+    int bc7_ranks;       /* shake-rank cap (0 = reference) */
     int next;            /* next job (slice*nrows + row) */
     int njobs;
     pthread_mutex_t lock;
@@ -83,6 +84,16 @@ static void encode_row(job_t *j, uint32_t slice, uint32_t brow)
             /* Image_CompressAMDBC1 defaults: steps 1, threshold 128/255 */
             orc_bc1_block(blk, 1, 128 / 255.0f, o);
             break;
+        case 2:
+        case 3:
+            /* amd_bc{2,3}_compressor.cpp:36-50: alpha half, then the colour half */
+            for (int i = 0; i < 16; ++i) ch[i] = blk[i * 4 + 3];
+            if (j->fmt == 3)
+                orc_bc4_block(ch, o);
+            else
+                orc_explicit_alpha_block(ch, o);
+            orc_rgb4_block(blk, 1, o + 8);
+            break;
         case 4:
             for (int i = 0; i < 16; ++i) ch[i] = blk[i * 4 + j->bc4_channel];
             orc_bc4_block(ch, o);
@@ -95,7 +106,7 @@ static void encode_row(job_t *j, uint32_t slice, uint32_t brow)
             break;
         case 7:
             /* Image_CompressAMDBC7 (amd_bc7_compressor.cpp:58-65) */
-            e = orc_bc7_block(blk, j->bc7_mask, has_alpha, j->bc7_quality, 1, 1, 1.0f, o);
+            e = orc_bc7_block_ex(blk, j->bc7_mask, has_alpha, j->bc7_quality, 1, 1, 1.0f, j->bc7_ranks, o);
             break;
         }
         if (j->err) j->err[out_row + bx] = e;
@@ -117,10 +128,10 @@ static void *worker(void *arg)
 
 static int encode_image(int fmt, const uint8_t *src, uint32_t width, uint32_t height, uint32_t slices,
                         uint32_t channels, int bc4_channel, int32_t first_row, int32_t num_rows, int threads,
-                        float bc7_quality, uint8_t bc7_mask, uint8_t *dst, double *block_err)
+                        float bc7_quality, uint8_t bc7_mask, int bc7_ranks, uint8_t *dst, double *block_err)
 {
     if (!src || !dst || !width || !height || !slices || channels < 1 || channels > 4) return -1;
-    if (fmt != 1 && fmt != 4 && fmt != 5 && fmt != 7) return -1;
+    if (fmt < 1 || fmt > 7 || fmt == 6) return -1;
     job_t j;
     memset(&j, 0, sizeof(j));
     j.fmt = fmt;
@@ -132,6 +143,7 @@ static int encode_image(int fmt, const uint8_t *src, uint32_t width, uint32_t he
     j.bc4_channel = bc4_channel;
     j.bc7_quality = bc7_quality;
     j.bc7_mask = bc7_mask;
+    j.bc7_ranks = bc7_ranks;
     j.bx_count = (width + 3) / 4;
     j.by_count = (height + 3) / 4;
     j.row0 = first_row < 0 ? 0 : (uint32_t)first_row;
@@ -158,7 +170,7 @@ int orc_encode_image(int fmt, const uint8_t *src, uint32_t width, uint32_t heigh
                      int threads, uint8_t *dst, double *block_err)
 {
     return encode_image(fmt, src, width, height, slices, channels, bc4_channel, first_row, num_rows, threads, 1.0f,
-                        0xFF, dst, block_err);
+                        0xFF, 0, dst, block_err);
 }
 
 int orc_encode_image_bc7(const uint8_t *src, uint32_t width, uint32_t height, uint32_t slices, uint32_t channels,
@@ -166,5 +178,13 @@ int orc_encode_image_bc7(const uint8_t *src, uint32_t width, uint32_t height, ui
                          uint8_t *dst, double *block_err)
 {
     return encode_image(7, src, width, height, slices, channels, 0, first_row, num_rows, threads, quality,
-                        mode_mask, dst, block_err);
+                        mode_mask, 0, dst, block_err);
+}
+
+int orc_encode_image_bc7_ex(const uint8_t *src, uint32_t width, uint32_t height, uint32_t slices, uint32_t channels,
+                            int32_t first_row, int32_t num_rows, int threads, float quality, uint8_t mode_mask,
+                            int shake_ranks, uint8_t *dst, double *block_err)
+{
+    return encode_image(7, src, width, height, slices, channels, 0, first_row, num_rows, threads, quality,
+                        mode_mask, shake_ranks, dst, block_err);
 }

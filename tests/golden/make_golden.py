@@ -31,6 +31,10 @@ def cases():
     yield "bc4_g1_64_ch1", 4, synth.g1(64, 64), {"bc4_channel": 1}
     yield "bc5_g0_256", 5, synth.g0(256, 256), {}
     yield "bc5_normal_128", 5, synth.normal_map(synth.height_field(128, 128, seed=1)), {}
+    yield "bc3_noise_alpha_64", 3, synth.noise_rgba(64, 64, seed=9, alpha=True), {}
+    yield "bc3_pattern_alpha_32", 3, synth.reference_pattern_rgb(32, 32, alpha_ramp=True), {}
+    yield "bc2_pattern_alpha_32", 2, synth.reference_pattern_rgb(32, 32, alpha_ramp=True), {}
+    yield "bc2_g1_64", 2, synth.g1(64, 64), {}
     yield "bc7_g0_256_rows0_2", 7, synth.g0(256, 256), {"first_row": 0, "num_rows": 2}
     yield "bc7_g1_256_rows0_2", 7, synth.g1(256, 256), {"first_row": 0, "num_rows": 2}
     yield "bc7_pattern_alpha_16", 7, synth.reference_pattern_rgb(16, 16, alpha_ramp=True), {}

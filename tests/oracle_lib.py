@@ -37,8 +37,14 @@ def lib() -> ctypes.CDLL:
                                               ctypes.c_int32, ctypes.c_int32, ctypes.c_int, ctypes.c_float,
                                               ctypes.c_uint8, vp, vp]
         _lib.orc_encode_image_bc7.restype = ctypes.c_int
+        _lib.orc_encode_image_bc7_ex.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                 ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int,
+                                                 ctypes.c_float, ctypes.c_uint8, ctypes.c_int, vp, vp]
+        _lib.orc_encode_image_bc7_ex.restype = ctypes.c_int
         _lib.orc_bc1_block.argtypes = [vp, ctypes.c_int, ctypes.c_float, vp]
         _lib.orc_bc4_block.argtypes = [vp, vp]
+        _lib.orc_rgb4_block.argtypes = [vp, ctypes.c_int, vp]
+        _lib.orc_explicit_alpha_block.argtypes = [vp, vp]
         _lib.orc_bc7_block.argtypes = [vp, ctypes.c_uint8, ctypes.c_int, ctypes.c_float, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_float, vp]
         _lib.orc_bc7_block.restype = ctypes.c_double
@@ -77,8 +83,9 @@ def encode_image(fmt: int, img: np.ndarray, bc4_channel: int = 1, first_row: int
 
 
 def encode_image_bc7(img: np.ndarray, quality: float = 1.0, mode_mask: int = 0xFF, first_row: int = -1,
-                     num_rows: int = -1, threads: int = 0, want_err: bool = False):
-    """BC7 over an image with the encoder quality / ModeMask of the block API."""
+                     num_rows: int = -1, threads: int = 0, want_err: bool = False, shake_ranks: int = 0):
+    """BC7 over an image with the encoder quality / ModeMask of the block API;
+    shake_ranks > 0 models the GPU's pruned search (gic_options.bc7_shake_ranks)."""
     a = np.ascontiguousarray(img, dtype=np.uint8)
     if a.ndim == 2:
         a = a[:, :, None]
@@ -90,8 +97,8 @@ def encode_image_bc7(img: np.ndarray, quality: float = 1.0, mode_mask: int = 0xF
     out = np.zeros((s * rows * bx, 16), np.uint8)
     err = np.zeros(s * rows * bx, np.float64) if want_err else None
     threads = threads or min(os.cpu_count() or 1, 16)
-    rc = lib().orc_encode_image_bc7(a.ctypes.data, w, h, s, c, first_row, num_rows, threads, quality, mode_mask,
-                                    out.ctypes.data, err.ctypes.data if want_err else None)
+    rc = lib().orc_encode_image_bc7_ex(a.ctypes.data, w, h, s, c, first_row, num_rows, threads, quality, mode_mask,
+                                       shake_ranks, out.ctypes.data, err.ctypes.data if want_err else None)
     if rc != 0:
         raise RuntimeError(f"oracle encode failed ({rc})")
     return (out, err) if want_err else out
@@ -108,6 +115,21 @@ def bc4_block(values: np.ndarray) -> bytes:
     v = np.ascontiguousarray(values, dtype=np.float32).reshape(16)
     out = np.zeros(8, np.uint8)
     lib().orc_bc4_block(v.ctypes.data, out.ctypes.data)
+    return out.tobytes()
+
+
+def bc23_block(fmt: int, block: np.ndarray, steps: int = 1) -> bytes:
+    """BC2 (fmt 2) / BC3 (fmt 3) block from 16 RGBA float texels: alpha half, colour half."""
+    b = np.ascontiguousarray(block, dtype=np.float32).reshape(64)
+    a = np.ascontiguousarray(b.reshape(16, 4)[:, 3])
+    out = np.zeros(16, np.uint8)
+    if fmt == 3:
+        lib().orc_bc4_block(a.ctypes.data, out.ctypes.data)
+    else:
+        lib().orc_explicit_alpha_block(a.ctypes.data, out.ctypes.data)
+    col = np.zeros(8, np.uint8)
+    lib().orc_rgb4_block(b.ctypes.data, steps, col.ctypes.data)
+    out[8:] = col
     return out.tobytes()
 
 
