@@ -469,7 +469,8 @@ def main():
     ch = CHANNELS[fmt]
     nblocks = bx * rows
     dst = torch.empty(nblocks * gic.block_bytes(fmt), dtype=torch.uint8, device=dev)
-    opts = gic.Options(bc4_channel=0, bc7_quality=args.bc7_quality)
+    opts = gic.Options(bc4_channel=0, bc7_quality=args.bc7_quality,
+                       bc7_shake_ranks=args.bc7_shake_ranks if fmt == 7 else 0)
     stream = torch.cuda.current_stream(dev)
 
     def step():

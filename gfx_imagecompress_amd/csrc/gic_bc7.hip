@@ -1141,6 +1141,7 @@ struct Params {
     // mode whose packed block decodes closest to the texels wins, not the one
     // with the least search error (DESIGN.md, BC7 pruned search)
     int decode_select;
+    int dual_cap;   // pruned search: dual-index candidates shaken per mode, 2 x bc7_shake_ranks (0 = the reference's gating)
 };
 
 // BlockMeta.flags bit 2: the block met the error threshold in an earlier
@@ -1684,11 +1685,25 @@ __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, c
 // CompressDualIndexBlock shakes a (rotation, selection) candidate when
 // quality > 0.7 or its quantiser error qe = e_colour + e_alpha / 3 is <= the
 // smallest qe of the mode's earlier candidates (:1141, :1170)
+// The pruned search (Params.dual_cap > 0) shakes only the dual_cap candidates
+// of least qe of the mode, ties to the earlier (rotation, selection).
 __device__ __forceinline__ bool dual_shaken(const Params &p, const Workspace &ws, uint32_t b, int task)
 {
-    if (p.quality > 0.7) return true;
     const int t0 = task < 8 ? 0 : 8;
     const double *q = ws.dqerr + (size_t)b * kDualTasks * 2;
+    if (p.dual_cap > 0) {
+        const int t1 = task < 8 ? 8 : 12;
+        double qt = q[2 * task];
+        qt += q[2 * task + 1] / 3.;
+        int rank = 0;
+        for (int t = t0; t < t1; ++t) {
+            double qe = q[2 * t];
+            qe += q[2 * t + 1] / 3.;
+            rank += (qe < qt || (qe == qt && t < task)) ? 1 : 0;
+        }
+        return rank < p.dual_cap;
+    }
+    if (p.quality > 0.7) return true;
     double best_q = 1.7976931348623157e308;
     for (int t = t0; t < task; ++t) {
         double qe = q[2 * t];
@@ -2314,6 +2329,7 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
         }
         p.att = host_attempts(p, o.bc7_shake_ranks);
         p.decode_select = o.bc7_shake_ranks > 0 && !(p.err_thr > 0);
+        p.dual_cap = 2 * (int)o.bc7_shake_ranks;
         const uint32_t wg = 256;
         if (g)
             hipLaunchKernelGGL(k_prep_image, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, *g, p, ws);

@@ -1080,6 +1080,7 @@ static double single_index(bc7_enc *e, double in[16][4], uint8_t out[16], int mo
             for (int k = 0; k < cnt[s]; ++k) e->stored[part][s][k] = idx[k];
         }
         e->stored_err[part] = err;
+        TRACE(4, mode, (int)part, (int)part, err, (const double *)0);
     }
     sort_order(e->stored_err, e->sorted, (int)tries);
 
@@ -1234,6 +1235,30 @@ static double dual_index(bc7_enc *e, double in[16][4], uint8_t out[16], int mode
     double cb[16][4], ab[16][4], best_q = DBL_MAX, best_o = DBL_MAX;
     int idx[2][16];
     double oq[2][16][4];
+    /* not in the reference: the GPU's pruned search (rank_cap > 0) shakes only
+     * the 2 * rank_cap candidates of least quantiser error (stable in (rot, sel)
+     * order); the quantiser results themselves are those of the main loop */
+    int qrank[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (e->rank_cap > 0) {
+        double qall[8];
+        for (int rot = 0; rot < nrot; ++rot) {
+            for (int i = 0; i < 16; ++i) {
+                cb[i][0] = in[i][kRot[rot][1]];
+                cb[i][1] = in[i][kRot[rot][2]];
+                cb[i][2] = in[i][kRot[rot][3]];
+                ab[i][0] = ab[i][1] = ab[i][2] = in[i][kRot[rot][0]];
+                cb[i][3] = ab[i][3] = 0.0;
+            }
+            for (int sel = 0; sel < nsel; ++sel) {
+                double q = opt_quant(cb, 16, 1 << ibs[sel], idx[0], oq[0], 3);
+                q += opt_quant(ab, 16, 1 << ibs[1 ^ sel], idx[1], oq[1], 3) / 3.;
+                qall[rot * nsel + sel] = q;
+            }
+        }
+        for (int t = 0; t < nrot * nsel; ++t)
+            for (int u = 0; u < nrot * nsel; ++u)
+                qrank[t] += (qall[u] < qall[t] || (qall[u] == qall[t] && u < t)) ? 1 : 0;
+    }
     for (int rot = 0; rot < nrot; ++rot) {
         for (int i = 0; i < 16; ++i) {
             cb[i][0] = in[i][kRot[rot][1]];
@@ -1250,7 +1275,7 @@ static double dual_index(bc7_enc *e, double in[16][4], uint8_t out[16], int mode
             }
             qe = opt_quant(cb, 16, 1 << ibs[sel], idx[0], oq[0], 3);
             qe += opt_quant(ab, 16, 1 << ibs[1 ^ sel], idx[1], oq[1], 3) / 3.;
-            if (e->quality > 0.7 || qe <= best_q) {
+            if (e->rank_cap > 0 ? qrank[rot * nsel + sel] < 2 * e->rank_cap : (e->quality > 0.7 || qe <= best_q)) {
                 unsigned shake = (unsigned)(6 * e->quality);
                 shake = shake < 6 ? shake : 6;
                 shake = shake > 2 ? shake : 2;

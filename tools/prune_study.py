@@ -44,13 +44,13 @@ def run(blocks, threads):
     lib = ctypes.CDLL(SO)
     n = blocks.shape[0]
     q = np.zeros((n, 8, 8)); s = np.zeros((n, 8, 8)); m = np.zeros((n, 8)); p = np.zeros((n, 8, 8), np.int32)
-    best = np.zeros(n); out = np.zeros((n, 16), np.uint8)
+    best = np.zeros(n); out = np.zeros((n, 16), np.uint8); allq = np.zeros((n, 8, 64))
     vp = ctypes.c_void_p
-    lib.study.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp, vp, vp, vp, vp]
+    lib.study.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp, vp, vp, vp, vp, vp]
     b = np.ascontiguousarray(blocks)
     lib.study(b.ctypes.data, n, threads, q.ctypes.data, s.ctypes.data, m.ctypes.data, p.ctypes.data,
-              best.ctypes.data, out.ctypes.data)
-    return dict(q=q, s=s, m=m, p=p, best=best, out=out)
+              best.ctypes.data, out.ctypes.data, allq.ctypes.data)
+    return dict(q=q, s=s, m=m, p=p, best=best, out=out, allq=allq)
 
 
 if __name__ == "__main__":
