@@ -21,7 +21,7 @@ from dataclasses import dataclass, replace
 
 __all__ = [
     "GicError", "Options", "FMT_BC1", "FMT_BC2", "FMT_BC3", "FMT_BC4", "FMT_BC5", "FMT_BC7", "library",
-    "block_bytes", "blocks_shape", "encode_device", "encode_blocks_f32", "compress_bc1", "compress_bc2",
+    "block_bytes", "blocks_shape", "encode_device", "encode_blocks_f32", "decode_device", "compress_bc1", "compress_bc2",
     "compress_bc3", "compress_bc4", "compress_bc5", "compress_bc7", "LIB_PATH",
 ]
 
@@ -117,6 +117,12 @@ def library() -> ctypes.CDLL:
     lib.gic_hip_encode.restype = ctypes.c_int
     lib.gic_hip_encode_blocks_f32.argtypes = [ctypes.c_int, vp, u32, ctypes.POINTER(_COptions), vp, vp, vp]
     lib.gic_hip_encode_blocks_f32.restype = ctypes.c_int
+    lib.gic_hip_decode.argtypes = [ctypes.c_int, vp, u32, u32, u32, vp, sz, vp]
+    lib.gic_hip_decode.restype = ctypes.c_int
+    lib.gic_decompress_image.argtypes = [vp]
+    lib.gic_decompress_image.restype = vp
+    lib.gic_save_dds.argtypes = [vp, ctypes.c_char_p]
+    lib.gic_save_dds.restype = ctypes.c_int
     lib.gic_default_options.argtypes = [ctypes.POINTER(_COptions)]
     lib.gic_default_options.restype = None
     lib.gic_block_bytes.argtypes = [ctypes.c_int]
@@ -213,6 +219,23 @@ def encode_blocks_f32(fmt: int, blocks, dst, options: Options | None = None, blo
                                              block_err.data_ptr() if block_err is not None else None,
                                              _stream_handle(stream))
     _check(rc)
+
+
+def decode_device(fmt: int, blocks, width: int, height: int, slices: int, out, row_pitch: int | None = None,
+                  stream=None) -> None:
+    """Asynchronously decode BCn blocks (uint8 CUDA tensor, row-major per slice)
+    into ``out`` (uint8 CUDA tensor of slices*height rows of row_pitch bytes,
+    RGBA8) -- gic_hip_decode."""
+    if not (blocks.is_cuda and out.is_cuda):
+        raise GicError("decode_device needs device (HBM) tensors; there is no CPU path")
+    bx, by = blocks_shape(width, height)
+    if blocks.numel() * blocks.element_size() < bx * by * slices * block_bytes(fmt):
+        raise GicError("blocks tensor too small for the given shape")
+    pitch = width * 4 if row_pitch is None else row_pitch
+    if not out.is_contiguous() or out.numel() * out.element_size() < pitch * height * slices:
+        raise GicError("out tensor too small for the given shape")
+    _check(library().gic_hip_decode(fmt, blocks.data_ptr(), width, height, slices, out.data_ptr(), pitch,
+                                    _stream_handle(stream)))
 
 
 def _host_compress(fmt: int, image, options: Options):

@@ -28,6 +28,10 @@ hipError_t launch_bc1_image(const Geometry &g, float thr, int steps, int force_a
 hipError_t launch_bc45_image(const Geometry &g, int fmt, int channel, void *dst, hipStream_t s);
 hipError_t launch_bc23_image(const Geometry &g, int fmt, int steps, int force_alpha_one, void *dst, hipStream_t s);
 hipError_t launch_bc23_blocks(const float *blocks, uint32_t n, int fmt, int steps, void *dst, hipStream_t s);
+hipError_t launch_bcx_decode(const uint8_t *blocks, int fmt, uint32_t width, uint32_t height, uint32_t slices,
+                             uint8_t *out, size_t row_pitch, hipStream_t s);
+hipError_t launch_bc7_decode(const uint8_t *blocks, uint32_t width, uint32_t height, uint32_t slices, uint8_t *out,
+                             size_t row_pitch, hipStream_t s);
 hipError_t launch_bc1_blocks(const float *blocks, uint32_t n, float thr, int steps, void *dst, hipStream_t s);
 hipError_t launch_bc4_blocks(const float *blocks, uint32_t n, void *dst, hipStream_t s);
 hipError_t launch_bc7_image(const Geometry &g, const gic_options &o, void *dst, double *err, hipStream_t s);
@@ -175,6 +179,19 @@ extern "C" int gic_hip_encode_blocks_f32(gic_format fmt, const float *d_blocks, 
         e = gic::launch_bc23_blocks(d_blocks, n, (int)fmt, o.refinement_steps, d_dst, s);
     else
         e = gic::launch_bc7_blocks(d_blocks, n, o, d_dst, d_block_err, s);
+    if (e != hipSuccess) return hip_fail(e);
+    return GIC_OK;
+}
+
+extern "C" int gic_hip_decode(gic_format fmt, const uint8_t *d_blocks, uint32_t width, uint32_t height,
+                              uint32_t slices, uint8_t *d_rgba, size_t row_pitch, void *stream)
+{
+    if (!valid_fmt(fmt) || !d_blocks || !d_rgba || !width || !height || !slices) return GIC_EINVAL;
+    if (row_pitch < (size_t)width * 4) return GIC_EINVAL;
+    const hipError_t e = fmt == GIC_FMT_BC7
+                             ? gic::launch_bc7_decode(d_blocks, width, height, slices, d_rgba, row_pitch, (hipStream_t)stream)
+                             : gic::launch_bcx_decode(d_blocks, (int)fmt, width, height, slices, d_rgba, row_pitch,
+                                                      (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e);
     return GIC_OK;
 }
@@ -553,6 +570,106 @@ extern "C" Image_CompressType ImageCompress_PickCompressionType(Image_CompressPi
         if (flags & Image_CPF_AllowETC) return Image_CT_None;
     }
     return Image_CT_None;
+}
+
+// ---- extensions: GPU decode of a compressed host image, DDS writer
+
+static gic_format block_format_of(TinyImageFormat f)
+{
+    switch (f) {
+    case TinyImageFormat_DXBC1_RGB_UNORM:
+    case TinyImageFormat_DXBC1_RGB_SRGB:
+    case TinyImageFormat_DXBC1_RGBA_UNORM:
+    case TinyImageFormat_DXBC1_RGBA_SRGB: return GIC_FMT_BC1;
+    case TinyImageFormat_DXBC2_UNORM:
+    case TinyImageFormat_DXBC2_SRGB: return GIC_FMT_BC2;
+    case TinyImageFormat_DXBC3_UNORM:
+    case TinyImageFormat_DXBC3_SRGB: return GIC_FMT_BC3;
+    case TinyImageFormat_DXBC4_UNORM:
+    case TinyImageFormat_DXBC4_SNORM: return GIC_FMT_BC4;
+    case TinyImageFormat_DXBC5_UNORM:
+    case TinyImageFormat_DXBC5_SNORM: return GIC_FMT_BC5;
+    case TinyImageFormat_DXBC7_UNORM:
+    case TinyImageFormat_DXBC7_SRGB: return GIC_FMT_BC7;
+    default: return (gic_format)0;
+    }
+}
+
+extern "C" Image_ImageHeader const *gic_decompress_image(Image_ImageHeader const *src)
+{
+    if (!src || !src->data) return nullptr;
+    const gic_format fmt = block_format_of(src->format);
+    if (!fmt) return nullptr;
+    Image_ImageHeader const *dst =
+        Image_CreateNoClear(src->width, src->height, 1, src->slices,
+                            TinyImageFormat_IsSRGB(src->format) ? TinyImageFormat_R8G8B8A8_SRGB
+                                                                : TinyImageFormat_R8G8B8A8_UNORM);
+    if (!dst) return nullptr;
+    const size_t blocks_bytes = (size_t)((src->width + 3) / 4) * ((src->height + 3) / 4) * src->slices *
+                                gic_block_bytes(fmt);
+    DeviceScratch &s = t_scratch;
+    const bool ok = s.reserve(blocks_bytes, dst->dataSize) &&
+                    hipMemcpyAsync(s.src, src->data, blocks_bytes, hipMemcpyHostToDevice, s.stream) == hipSuccess &&
+                    gic_hip_decode(fmt, (const uint8_t *)s.src, src->width, src->height, src->slices,
+                                   (uint8_t *)s.dst, (size_t)src->width * 4, s.stream) == GIC_OK &&
+                    hipMemcpyAsync(dst->data, s.dst, dst->dataSize, hipMemcpyDeviceToHost, s.stream) == hipSuccess &&
+                    hipStreamSynchronize(s.stream) == hipSuccess;
+    if (!ok) {
+        Image_Destroy(dst);
+        return nullptr;
+    }
+    return dst;
+}
+
+// DDS: "DDS " + DDS_HEADER (124 bytes) [+ DDS_HEADER_DXT10 (20 bytes)] + data
+extern "C" int gic_save_dds(Image_ImageHeader const *img, const char *path)
+{
+    if (!img || !img->data || !path) return GIC_EINVAL;
+    const gic_format fmt = block_format_of(img->format);
+    if (!fmt) return GIC_EINVAL;
+    const bool srgb = TinyImageFormat_IsSRGB(img->format);
+    const bool snorm = img->format == TinyImageFormat_DXBC4_SNORM || img->format == TinyImageFormat_DXBC5_SNORM;
+    const bool dx10 = fmt == GIC_FMT_BC7 || srgb || snorm || img->slices > 1;
+    // DXGI_FORMAT values of the DX10 header
+    uint32_t dxgi = 0;
+    switch (fmt) {
+    case GIC_FMT_BC1: dxgi = srgb ? 72 : 71; break;
+    case GIC_FMT_BC2: dxgi = srgb ? 75 : 74; break;
+    case GIC_FMT_BC3: dxgi = srgb ? 78 : 77; break;
+    case GIC_FMT_BC4: dxgi = snorm ? 81 : 80; break;
+    case GIC_FMT_BC5: dxgi = snorm ? 84 : 83; break;
+    case GIC_FMT_BC7: dxgi = srgb ? 99 : 98; break;
+    }
+    const uint32_t bb = gic_block_bytes(fmt);
+    const uint32_t bx = (img->width + 3) / 4, by = (img->height + 3) / 4;
+    uint32_t h[31];
+    memset(h, 0, sizeof(h));
+    h[0] = 124;                                   // dwSize
+    h[1] = 0x1 | 0x2 | 0x4 | 0x1000 | 0x80000;    // CAPS | HEIGHT | WIDTH | PIXELFORMAT | LINEARSIZE
+    h[2] = img->height;
+    h[3] = img->width;
+    h[4] = bx * bb;                               // pitch of a block row
+    h[6] = 1;                                     // mip levels
+    h[18] = 32;                                   // DDS_PIXELFORMAT.dwSize
+    h[19] = 0x4;                                  // DDPF_FOURCC
+    auto fourcc = [](const char *c) {
+        return (uint32_t)c[0] | ((uint32_t)c[1] << 8) | ((uint32_t)c[2] << 16) | ((uint32_t)c[3] << 24);
+    };
+    h[20] = dx10 ? fourcc("DX10")
+                 : fourcc(fmt == GIC_FMT_BC1 ? "DXT1" : fmt == GIC_FMT_BC2 ? "DXT3" : fmt == GIC_FMT_BC3 ? "DXT5"
+                                                     : fmt == GIC_FMT_BC4 ? "ATI1" : "ATI2");
+    h[26] = 0x1000;                               // DDSCAPS_TEXTURE
+    FILE *f = fopen(path, "wb");
+    if (!f) return GIC_EHIP;
+    bool ok = fwrite("DDS ", 1, 4, f) == 4 && fwrite(h, 4, 31, f) == 31;
+    if (ok && dx10) {
+        const uint32_t x[5] = {dxgi, 3 /* TEXTURE2D */, 0, img->slices, 0};
+        ok = fwrite(x, 4, 5, f) == 5;
+    }
+    const size_t bytes = (size_t)bx * by * img->slices * bb;
+    ok = ok && fwrite(img->data, 1, bytes, f) == bytes;
+    ok = (fclose(f) == 0) && ok;
+    return ok ? GIC_OK : GIC_EHIP;
 }
 
 // ---- block level: one-block GPU launches (prefer gic_hip_encode_blocks_f32 for batches)

@@ -2366,6 +2366,55 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
 
 }  // namespace bc7
 
+namespace bc7 {
+__global__ void __launch_bounds__(256) k_decode(const uint4 *__restrict__ blocks, uint32_t width, uint32_t height,
+                                                uint32_t bx_count, uint32_t total, uint8_t *__restrict__ out,
+                                                size_t row_pitch)
+{
+    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= total) return;
+    const uint32_t by_count = (height + 3) / 4;
+    const uint32_t bx = id % bx_count, r = id / bx_count, by = r % by_count, slice = r / by_count;
+    const uint4 b = blocks[id];
+    const uint32_t w[4] = {b.x, b.y, b.z, b.w};
+    uint32_t px[16];
+    bc7_decode_block(w, px);
+    uint8_t *img = out + (size_t)slice * row_pitch * height;
+    const uint32_t x0 = bx * 4, y0 = by * 4;
+    const bool whole = x0 + 4 <= width && y0 + 4 <= height && ((row_pitch | (uintptr_t)out) & 15) == 0;
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+        if (y0 + y >= height) break;
+        uint8_t *row = img + (size_t)(y0 + y) * row_pitch + (size_t)x0 * 4;
+        if (whole) {
+            *reinterpret_cast<uint4 *>(row) = make_uint4(px[4 * y], px[4 * y + 1], px[4 * y + 2], px[4 * y + 3]);
+        } else {
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+                if (x0 + x < width) *reinterpret_cast<uint32_t *>(row + 4 * x) = px[4 * y + x];
+        }
+    }
+}
+}  // namespace bc7
+
+hipError_t launch_bc7_decode(const uint8_t *blocks, uint32_t width, uint32_t height, uint32_t slices, uint8_t *out,
+                             size_t row_pitch, hipStream_t s)
+{
+    {   // the partition / anchor tables live in this library's constant memory
+        std::lock_guard<std::mutex> lk(bc7::g_state_lock);
+        bc7::DeviceState *st = nullptr;
+        const hipError_t e = bc7::get_state(0, 0, st);
+        if (e != hipSuccess) return e;
+    }
+    const uint32_t bx = (width + 3) / 4, by = (height + 3) / 4;
+    const uint64_t total = (uint64_t)bx * by * slices;
+    if (total > 0xffffffffull) return hipErrorInvalidValue;
+    const uint32_t wg = 256, grid = (uint32_t)((total + wg - 1) / wg);
+    hipLaunchKernelGGL(bc7::k_decode, dim3(grid), dim3(wg), 0, s, (const uint4 *)blocks, width, height, bx,
+                       (uint32_t)total, out, row_pitch);
+    return hipGetLastError();
+}
+
 hipError_t launch_bc7_image(const Geometry &g, const gic_options &o, void *dst, double *err, hipStream_t s)
 {
     return bc7::run_chunks(&g, nullptr, g.total, o, dst, err, s);

@@ -1167,7 +1167,140 @@ __global__ void __launch_bounds__(256) bc23_blocks_kernel(const float *__restric
     dst[id] = make_uint4(a.x, a.y, c.x, c.y);
 }
 
+// ------------------------------------------------------------- decode ---
+
+namespace dec {
+
+__device__ __forceinline__ void rgb565(uint32_t c, int v[3])
+{
+    const int r = (int)(c >> 11) & 31, g = (int)(c >> 5) & 63, b = (int)c & 31;
+    v[0] = (r << 3) | (r >> 2);
+    v[1] = (g << 2) | (g >> 4);
+    v[2] = (b << 3) | (b >> 2);
+}
+
+// colour block (8 bytes) -> 16 packed RGBA words; four_only: BC2/BC3
+__device__ __forceinline__ void colour_block(uint2 blk, bool four_only, uint32_t px[16])
+{
+    const uint32_t c0 = blk.x & 0xffffu, c1 = blk.x >> 16;
+    int e0[3], e1[3];
+    rgb565(c0, e0);
+    rgb565(c1, e1);
+    const bool four = four_only || c0 > c1;
+    uint32_t pal[4];
+    pal[0] = (uint32_t)e0[0] | ((uint32_t)e0[1] << 8) | ((uint32_t)e0[2] << 16) | 0xff000000u;
+    pal[1] = (uint32_t)e1[0] | ((uint32_t)e1[1] << 8) | ((uint32_t)e1[2] << 16) | 0xff000000u;
+    pal[2] = pal[3] = 0xff000000u;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const uint32_t v2 = four ? (uint32_t)(2 * e0[c] + e1[c] + 1) / 3 : (uint32_t)(e0[c] + e1[c] + 1) / 2;
+        const uint32_t v3 = four ? (uint32_t)(e0[c] + 2 * e1[c] + 1) / 3 : 0u;
+        pal[2] |= v2 << (8 * c);
+        pal[3] |= v3 << (8 * c);
+    }
+    if (!four) pal[3] = 0u;   // transparent black
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t k = (blk.y >> (2 * i)) & 3u;
+        px[i] = k == 0 ? pal[0] : (k == 1 ? pal[1] : (k == 2 ? pal[2] : pal[3]));
+    }
+}
+
+// BC4 block -> 16 values
+__device__ __forceinline__ void scalar_block(uint2 blk, uint32_t v[16])
+{
+    const int e0 = (int)(blk.x & 0xffu), e1 = (int)((blk.x >> 8) & 0xffu);
+    const uint64_t bits = ((uint64_t)blk.x | ((uint64_t)blk.y << 32)) >> 16;
+    const bool eight = e0 > e1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int k = (int)((bits >> (3 * i)) & 7u);
+        int r;
+        if (k == 0)
+            r = e0;
+        else if (k == 1)
+            r = e1;
+        else if (eight)
+            r = ((8 - k) * e0 + (k - 1) * e1 + 3) / 7;
+        else
+            r = k == 6 ? 0 : (k == 7 ? 255 : ((6 - k) * e0 + (k - 1) * e1 + 2) / 5);
+        v[i] = (uint32_t)r;
+    }
+}
+
+}  // namespace dec
+
+// One lane per block; a block's four rows are written as 16-byte stores
+// (adjacent lanes = adjacent blocks: coalesced row segments) when whole.
+__global__ void __launch_bounds__(256) bcx_decode_kernel(const uint8_t *__restrict__ blocks, int fmt, uint32_t width,
+                                                         uint32_t height, uint32_t bx_count, uint32_t total,
+                                                         uint8_t *__restrict__ out, size_t row_pitch)
+{
+    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= total) return;
+    const uint32_t by_count = (height + 3) / 4;
+    const uint32_t bx = id % bx_count, r = id / bx_count, by = r % by_count, slice = r / by_count;
+    uint32_t px[16];
+    if (fmt == 1) {
+        dec::colour_block(reinterpret_cast<const uint2 *>(blocks)[id], false, px);
+    } else if (fmt == 4) {
+        uint32_t v[16];
+        dec::scalar_block(reinterpret_cast<const uint2 *>(blocks)[id], v);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) px[i] = v[i] | 0xff000000u;
+    } else {
+        const uint4 b = reinterpret_cast<const uint4 *>(blocks)[id];
+        if (fmt == 5) {
+            uint32_t v[16], w[16];
+            dec::scalar_block(make_uint2(b.x, b.y), v);
+            dec::scalar_block(make_uint2(b.z, b.w), w);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) px[i] = v[i] | (w[i] << 8) | 0xff000000u;
+        } else {
+            dec::colour_block(make_uint2(b.z, b.w), true, px);
+            if (fmt == 3) {
+                uint32_t a[16];
+                dec::scalar_block(make_uint2(b.x, b.y), a);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) px[i] = (px[i] & 0x00ffffffu) | (a[i] << 24);
+            } else {
+                const uint64_t ab = (uint64_t)b.x | ((uint64_t)b.y << 32);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) px[i] = (px[i] & 0x00ffffffu) | ((uint32_t)((ab >> (4 * i)) & 15u) * 17u << 24);
+            }
+        }
+    }
+    uint8_t *img = out + (size_t)slice * row_pitch * height;
+    const uint32_t x0 = bx * 4, y0 = by * 4;
+    const bool whole = x0 + 4 <= width && y0 + 4 <= height && ((row_pitch | (uintptr_t)out) & 15) == 0;
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+        if (y0 + y >= height) break;
+        uint8_t *row = img + (size_t)(y0 + y) * row_pitch + (size_t)x0 * 4;
+        if (whole) {
+            *reinterpret_cast<uint4 *>(row) = make_uint4(px[4 * y], px[4 * y + 1], px[4 * y + 2], px[4 * y + 3]);
+        } else {
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+                if (x0 + x < width) *reinterpret_cast<uint32_t *>(row + 4 * x) = px[4 * y + x];
+        }
+    }
+}
+
 // ------------------------------------------------------------ launchers ---
+
+hipError_t launch_bcx_decode(const uint8_t *blocks, int fmt, uint32_t width, uint32_t height, uint32_t slices,
+                             uint8_t *out, size_t row_pitch, hipStream_t s)
+{
+    const uint32_t bx = (width + 3) / 4, by = (height + 3) / 4;
+    const uint64_t total = (uint64_t)bx * by * slices;
+    if (total > 0xffffffffull) return hipErrorInvalidValue;
+    const uint32_t wg = 256, grid = (uint32_t)((total + wg - 1) / wg);
+    hipLaunchKernelGGL(bcx_decode_kernel, dim3(grid), dim3(wg), 0, s, blocks, fmt, width, height, bx, (uint32_t)total,
+                       out, row_pitch);
+    return hipGetLastError();
+}
+
 
 // smallest alpha byte passing `pass(a)` (256 if none); pass is monotone in a
 template <class F>

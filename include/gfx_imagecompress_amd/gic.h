@@ -83,12 +83,41 @@ int gic_hip_encode_rows(gic_format fmt, const uint8_t *d_src, uint32_t width, ui
                         uint8_t *d_dst, double *d_block_err, void *stream);
 
 /* Block-level batch: n blocks of 16 texels, float in [0,1].
- *   BC1/BC7: d_blocks holds n x 64 floats (RGBA per texel, texel-major).
+ *   BC1/BC2/BC3/BC7: d_blocks holds n x 64 floats (RGBA per texel, texel-major).
  *   BC4:     d_blocks holds n x 16 floats.
  * This is the batched form of the reference's block API
  * (imagecompress.h:111-136). */
 int gic_hip_encode_blocks_f32(gic_format fmt, const float *d_blocks, uint32_t n, const gic_options *opt,
                               uint8_t *d_dst, double *d_block_err, void *stream);
+
+/* Decode BCn blocks resident in HBM (row-major per slice, slices stacked, as
+ * the encoders write them) to RGBA8: d_rgba receives slices x height rows of
+ * row_pitch bytes, 4 bytes per texel (texels past the image edge are not
+ * written).  Conventions (not part of the reference, which has no decoder):
+ *   BC1/BC2/BC3 colour: 565 endpoints widened by bit replication, the 1/3 and
+ *     2/3 points rounded to nearest; BC1 with c0 <= c1 is the 3-colour mode
+ *     (midpoint rounded half up, index 3 = transparent black); BC2/BC3 colour
+ *     blocks are always 4-colour;
+ *   BC2 alpha: a4 * 17; BC3/BC4/BC5: the 8- or 6-level ramps rounded to
+ *     nearest; BC4 -> (R, 0, 0, 255), BC5 -> (R, G, 0, 255);
+ *   BC7: the BPTC format (weights round(64 i / (2^bits - 1)), reserved mode ->
+ *     transparent black). */
+int gic_hip_decode(gic_format fmt, const uint8_t *d_blocks, uint32_t width, uint32_t height, uint32_t slices,
+                   uint8_t *d_rgba, size_t row_pitch, void *stream);
+
+/* Host image helpers (extensions; the reference has neither):
+ *   gic_decompress_image: a BC1/BC2/BC3/BC4/BC5/BC7 image (as the
+ *     Image_CompressAMD* functions return) decoded on the GPU to an RGBA8
+ *     image (R8G8B8A8_SRGB for sRGB block formats), freed with Image_Destroy;
+ *     NULL for other formats or on failure.
+ *   gic_save_dds: writes a block-compressed image as a .dds file (legacy
+ *     DXT1/DXT3/DXT5/ATI1/ATI2 FourCC header, DX10 extension header for BC7 and
+ *     the sRGB variants) -- the SAVE_DDS step of the reference tests
+ *     (tests/test_imagecompress.cpp:9-26, which use gfx_imageio).  Returns 0 or
+ *     GIC_EINVAL / GIC_EHIP (I/O failure). */
+struct Image_ImageHeader;
+struct Image_ImageHeader const *gic_decompress_image(struct Image_ImageHeader const *src);
+int gic_save_dds(struct Image_ImageHeader const *img, const char *path);
 
 /* Last HIP error code recorded by this thread (0 if none). */
 int gic_last_hip_error(void);

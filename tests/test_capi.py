@@ -78,3 +78,36 @@ def test_image_model_and_pick_type():
     assert lib.ImageCompress_PickCompressionType(0x10, q) == 7  # DXBC7 when allowed
     assert lib.ImageCompress_PickCompressionType(0x1, q) == 3   # DXBC3 for alpha sources
     lib.Image_Destroy(q)
+
+
+def test_dds_writer_headers(tmp_path):
+    """gic_save_dds (host only): legacy FourCC header for BC1, DX10 header for
+    BC7 with the DXGI format, block data verbatim after the header."""
+    import struct
+    lib = gic.library()
+    lib.Image_CreateNoClear.restype = ctypes.c_void_p
+    lib.Image_Destroy.argtypes = [ctypes.c_void_p]
+    lib.Image_RawDataPtr.argtypes = [ctypes.c_void_p]
+    lib.Image_RawDataPtr.restype = ctypes.c_void_p
+    for fmt_id, want_fourcc, dxgi, bb in ((10, b"DXT1", None, 8), (18, b"DX10", 98, 16), (19, b"DX10", 99, 16)):
+        p = lib.Image_CreateNoClear(20, 12, 1, 1, fmt_id)
+        n = 5 * 3 * bb
+        payload = bytes((i * 7) & 255 for i in range(n))
+        ctypes.memmove(lib.Image_RawDataPtr(p), payload, n)
+        path = str(tmp_path / f"t{fmt_id}.dds")
+        assert lib.gic_save_dds(p, path.encode()) == gic.GIC_OK
+        data = open(path, "rb").read()
+        assert data[:4] == b"DDS "
+        size, flags, h, w, pitch = struct.unpack_from("<5I", data, 4)
+        assert (size, h, w, pitch) == (124, 12, 20, 5 * bb)
+        assert data[4 + 80:4 + 84] == want_fourcc
+        off = 128
+        if dxgi is not None:
+            assert struct.unpack_from("<5I", data, 128)[:2] == (dxgi, 3)
+            off += 20
+        assert data[off:] == payload
+        lib.Image_Destroy(p)
+    # not a block format
+    q = lib.Image_CreateNoClear(8, 8, 1, 1, 7)
+    assert lib.gic_save_dds(q, str(tmp_path / "x.dds").encode()) == gic.GIC_EINVAL
+    lib.Image_Destroy(q)
