@@ -21,7 +21,7 @@ from dataclasses import dataclass, replace
 
 __all__ = [
     "GicError", "Options", "FMT_BC1", "FMT_BC2", "FMT_BC3", "FMT_BC4", "FMT_BC5", "FMT_BC7", "library",
-    "block_bytes", "blocks_shape", "encode_device", "encode_blocks_f32", "decode_device", "compress_bc1", "compress_bc2",
+    "block_bytes", "blocks_shape", "encode_device", "encode_device_src", "encode_blocks_f32", "decode_device", "compress_bc1", "compress_bc2",
     "compress_bc3", "compress_bc4", "compress_bc5", "compress_bc7", "LIB_PATH",
 ]
 
@@ -112,6 +112,9 @@ def library() -> ctypes.CDLL:
     lib.gic_hip_encode_rows.argtypes = [ctypes.c_int, vp, u32, u32, u32, u32, sz, u32, u32,
                                         ctypes.POINTER(_COptions), vp, vp, vp]
     lib.gic_hip_encode_rows.restype = ctypes.c_int
+    lib.gic_hip_encode_rows_src.argtypes = [ctypes.c_int, ctypes.c_int, vp, u32, u32, u32, u32, sz, u32, u32,
+                                            ctypes.POINTER(_COptions), vp, vp, vp]
+    lib.gic_hip_encode_rows_src.restype = ctypes.c_int
     lib.gic_hip_encode.argtypes = [ctypes.c_int, vp, u32, u32, u32, u32, sz,
                                    ctypes.POINTER(_COptions), vp, vp, vp]
     lib.gic_hip_encode.restype = ctypes.c_int
@@ -187,6 +190,37 @@ def encode_device(fmt: int, src, width: int, height: int, slices: int, channels:
                                        first_block_row, nrows, ctypes.byref(opts), dst.data_ptr(),
                                        block_err.data_ptr() if block_err is not None else None,
                                        _stream_handle(stream))
+    _check(rc)
+
+
+SRC_UNORM8, SRC_SNORM8, SRC_FLOAT32 = 0, 1, 2
+
+
+def encode_device_src(fmt: int, src_type: int, src, width: int, height: int, slices: int, channels: int, dst,
+                      options: Options | None = None, first_block_row: int = 0, num_block_rows: int | None = None,
+                      block_err=None, stream=None) -> None:
+    """gic_hip_encode_rows_src: like :func:`encode_device` for SNORM8 (int8
+    tensor) or FLOAT32 (float32 tensor) sources, rows packed without padding."""
+    import torch
+    if not (src.is_cuda and dst.is_cuda):
+        raise GicError("encode_device_src needs device (HBM) tensors; there is no CPU path")
+    want = {SRC_UNORM8: torch.uint8, SRC_SNORM8: torch.int8, SRC_FLOAT32: torch.float32}[src_type]
+    if src.dtype != want or not src.is_contiguous():
+        raise GicError(f"source must be a contiguous {want} tensor for source type {src_type}")
+    bx, by = blocks_shape(width, height)
+    nrows = by - first_block_row if num_block_rows is None else num_block_rows
+    if src.numel() < width * height * slices * channels:
+        raise GicError("src too small for the given shape")
+    if dst.numel() * dst.element_size() < bx * nrows * slices * block_bytes(fmt):
+        raise GicError("dst too small")
+    if block_err is not None and (block_err.dtype != torch.float64 or block_err.numel() < bx * nrows * slices):
+        raise GicError("block_err must be float64 with one entry per block")
+    opts = (options or Options()).to_c()
+    rc = library().gic_hip_encode_rows_src(fmt, src_type, src.data_ptr(), width, height, slices, channels,
+                                           width * channels * src.element_size(), first_block_row, nrows,
+                                           ctypes.byref(opts), dst.data_ptr(),
+                                           block_err.data_ptr() if block_err is not None else None,
+                                           _stream_handle(stream))
     _check(rc)
 
 

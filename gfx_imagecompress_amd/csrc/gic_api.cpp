@@ -24,15 +24,20 @@
 #include "gic_common.h"
 
 namespace gic {
-hipError_t launch_bc1_image(const Geometry &g, float thr, int steps, int force_alpha_one, void *dst, hipStream_t s);
+hipError_t launch_bc1_image(const Geometry &g, float thr, int steps, int force_alpha_one, int r3d, void *dst,
+                            hipStream_t s);
 hipError_t launch_bc45_image(const Geometry &g, int fmt, int channel, void *dst, hipStream_t s);
-hipError_t launch_bc23_image(const Geometry &g, int fmt, int steps, int force_alpha_one, void *dst, hipStream_t s);
-hipError_t launch_bc23_blocks(const float *blocks, uint32_t n, int fmt, int steps, void *dst, hipStream_t s);
+hipError_t launch_bc23_image(const Geometry &g, int fmt, int steps, int force_alpha_one, int r3d, void *dst,
+                             hipStream_t s);
+hipError_t launch_bc23_blocks(const float *blocks, uint32_t n, int fmt, int steps, int r3d, void *dst, hipStream_t s);
+hipError_t launch_gather_f32(const Geometry &g, int kind, int force_alpha_one, uint32_t first, uint32_t n, float *out,
+                             hipStream_t s);
+hipError_t launch_bc45_rgba_blocks(const float *blocks, uint32_t n, int fmt, int channel, void *dst, hipStream_t s);
 hipError_t launch_bcx_decode(const uint8_t *blocks, int fmt, uint32_t width, uint32_t height, uint32_t slices,
                              uint8_t *out, size_t row_pitch, hipStream_t s);
 hipError_t launch_bc7_decode(const uint8_t *blocks, uint32_t width, uint32_t height, uint32_t slices, uint8_t *out,
                              size_t row_pitch, hipStream_t s);
-hipError_t launch_bc1_blocks(const float *blocks, uint32_t n, float thr, int steps, void *dst, hipStream_t s);
+hipError_t launch_bc1_blocks(const float *blocks, uint32_t n, float thr, int steps, int r3d, void *dst, hipStream_t s);
 hipError_t launch_bc4_blocks(const float *blocks, uint32_t n, void *dst, hipStream_t s);
 hipError_t launch_bc7_image(const Geometry &g, const gic_options &o, void *dst, double *err, hipStream_t s);
 hipError_t launch_bc7_blocks(const float *blocks, uint32_t n, const gic_options &o, void *dst, double *err,
@@ -74,7 +79,7 @@ extern "C" uint32_t gic_block_bytes(gic_format fmt)
 
 static int check_options(gic_format fmt, const gic_options &o)
 {
-    if (o.b3d_refinement || o.adaptive_weights) return GIC_EUNSUP;
+    if (o.adaptive_weights) return GIC_EUNSUP;
     if (o.refinement_steps > 8) return GIC_EINVAL;
     if (fmt == GIC_FMT_BC4 && o.bc4_channel > 3) return GIC_EINVAL;
     if (fmt == GIC_FMT_BC7 && o.bc7_performance != 1.0f) return GIC_EUNSUP;   // optQuantTrace_d path not built
@@ -128,11 +133,12 @@ extern "C" int gic_hip_encode_rows(gic_format fmt, const uint8_t *d_src, uint32_
     }
     switch (fmt) {
     case GIC_FMT_BC1:
-        e = gic::launch_bc1_image(g, o.bc1_alpha_threshold, o.refinement_steps, o.force_alpha_one, d_dst, s);
+        e = gic::launch_bc1_image(g, o.bc1_alpha_threshold, o.refinement_steps, o.force_alpha_one, o.b3d_refinement,
+                                  d_dst, s);
         break;
     case GIC_FMT_BC2:
     case GIC_FMT_BC3:
-        e = gic::launch_bc23_image(g, (int)fmt, o.refinement_steps, o.force_alpha_one, d_dst, s);
+        e = gic::launch_bc23_image(g, (int)fmt, o.refinement_steps, o.force_alpha_one, o.b3d_refinement, d_dst, s);
         break;
     case GIC_FMT_BC4:
     case GIC_FMT_BC5:
@@ -142,6 +148,79 @@ extern "C" int gic_hip_encode_rows(gic_format fmt, const uint8_t *d_src, uint32_
         e = gic::launch_bc7_image(g, o, d_dst, d_block_err, s);
         break;
     }
+    if (e != hipSuccess) return hip_fail(e);
+    return GIC_OK;
+}
+
+extern "C" int gic_hip_encode_rows_src(gic_format fmt, gic_source src_type, const void *d_src, uint32_t width,
+                                       uint32_t height, uint32_t slices, uint32_t channels, size_t row_pitch,
+                                       uint32_t first_block_row, uint32_t num_block_rows, const gic_options *opt,
+                                       uint8_t *d_dst, double *d_block_err, void *stream)
+{
+    if (src_type == GIC_SRC_UNORM8)
+        return gic_hip_encode_rows(fmt, (const uint8_t *)d_src, width, height, slices, channels, row_pitch,
+                                   first_block_row, num_block_rows, opt, d_dst, d_block_err, stream);
+    if (src_type != GIC_SRC_SNORM8 && src_type != GIC_SRC_FLOAT32) return GIC_EINVAL;
+    const size_t texel = (size_t)channels * (src_type == GIC_SRC_FLOAT32 ? 4 : 1);
+    if (!valid_fmt(fmt) || !d_src || !d_dst || !width || !height || !slices || channels < 1 || channels > 4)
+        return GIC_EINVAL;
+    if (row_pitch < (size_t)width * texel) return GIC_EINVAL;
+    const uint32_t by_count = (height + 3) / 4;
+    if (first_block_row >= by_count || num_block_rows == 0 || first_block_row + num_block_rows > by_count)
+        return GIC_EINVAL;
+    gic_options o;
+    gic_default_options(&o);
+    if (opt) {
+        if (opt->struct_size != sizeof(gic_options)) return GIC_EINVAL;
+        o = *opt;
+    }
+    int rc = check_options(fmt, o);
+    if (rc) return rc;
+    const uint64_t total = (uint64_t)((width + 3) / 4) * num_block_rows * slices;
+    if (total > 0xffffffffull) return GIC_EINVAL;
+    gic::Geometry g;
+    g.src = (const uint8_t *)d_src;
+    g.width = width;
+    g.height = height;
+    g.slices = slices;
+    g.channels = channels;
+    g.row_pitch = row_pitch;
+    g.bx_count = (width + 3) / 4;
+    g.row0 = first_block_row;
+    g.nrows = num_block_rows;
+    g.total = (uint32_t)total;
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t chunk = total < (1u << 20) ? (uint32_t)total : (1u << 20);   // 256 MiB of float blocks
+    float *tmp = nullptr;
+    hipError_t e = hipMallocAsync((void **)&tmp, (size_t)chunk * 64 * sizeof(float), s);
+    if (e != hipSuccess) return hip_fail(e);
+    if (d_block_err && fmt != GIC_FMT_BC7) e = hipMemsetAsync(d_block_err, 0, sizeof(double) * total, s);
+    const uint32_t bb = gic_block_bytes(fmt);
+    const int force_alpha = o.force_alpha_one || channels < 4;
+    for (uint32_t first = 0; e == hipSuccess && first < (uint32_t)total; first += chunk) {
+        const uint32_t n = ((uint32_t)total - first) < chunk ? ((uint32_t)total - first) : chunk;
+        e = gic::launch_gather_f32(g, src_type == GIC_SRC_SNORM8 ? 1 : 2, force_alpha, first, n, tmp, s);
+        if (e != hipSuccess) break;
+        uint8_t *out = d_dst + (size_t)first * bb;
+        switch (fmt) {
+        case GIC_FMT_BC1:
+            e = gic::launch_bc1_blocks(tmp, n, o.bc1_alpha_threshold, o.refinement_steps, o.b3d_refinement, out, s);
+            break;
+        case GIC_FMT_BC2:
+        case GIC_FMT_BC3:
+            e = gic::launch_bc23_blocks(tmp, n, (int)fmt, o.refinement_steps, o.b3d_refinement, out, s);
+            break;
+        case GIC_FMT_BC4:
+        case GIC_FMT_BC5:
+            e = gic::launch_bc45_rgba_blocks(tmp, n, (int)fmt, o.bc4_channel, out, s);
+            break;
+        case GIC_FMT_BC7:
+            e = gic::launch_bc7_blocks(tmp, n, o, out, d_block_err ? d_block_err + first : nullptr, s);
+            break;
+        }
+    }
+    const hipError_t ef = hipFreeAsync(tmp, s);
+    if (e == hipSuccess) e = ef;
     if (e != hipSuccess) return hip_fail(e);
     return GIC_OK;
 }
@@ -172,11 +251,11 @@ extern "C" int gic_hip_encode_blocks_f32(gic_format fmt, const float *d_blocks, 
     hipStream_t s = (hipStream_t)stream;
     hipError_t e = hipSuccess;
     if (fmt == GIC_FMT_BC1)
-        e = gic::launch_bc1_blocks(d_blocks, n, o.bc1_alpha_threshold, o.refinement_steps, d_dst, s);
+        e = gic::launch_bc1_blocks(d_blocks, n, o.bc1_alpha_threshold, o.refinement_steps, o.b3d_refinement, d_dst, s);
     else if (fmt == GIC_FMT_BC4)
         e = gic::launch_bc4_blocks(d_blocks, n, d_dst, s);
     else if (fmt == GIC_FMT_BC2 || fmt == GIC_FMT_BC3)
-        e = gic::launch_bc23_blocks(d_blocks, n, (int)fmt, o.refinement_steps, d_dst, s);
+        e = gic::launch_bc23_blocks(d_blocks, n, (int)fmt, o.refinement_steps, o.b3d_refinement, d_dst, s);
     else
         e = gic::launch_bc7_blocks(d_blocks, n, o, d_dst, d_block_err, s);
     if (e != hipSuccess) return hip_fail(e);
@@ -365,13 +444,17 @@ static Image_ImageHeader const *encode_host_image(Image_ImageHeader const *src, 
 {
     if (!src || !src->data || src->depth > 1) return nullptr;
     const uint32_t ch = TinyImageFormat_ChannelCount(src->format);
-    if (!ch || TinyImageFormat_IsCompressed(src->format) || TinyImageFormat_IsFloat(src->format) ||
-        TinyImageFormat_IsSigned(src->format))
-        return nullptr;   // 8-bit UNORM/sRGB sources only
+    if (!ch || TinyImageFormat_IsCompressed(src->format)) return nullptr;
+    // texel encoding (Image_GetPixelAtF, block_utils.cpp:24-26): the encoders
+    // take any format the reference reads as floats
+    const gic_source st = TinyImageFormat_IsFloat(src->format)    ? GIC_SRC_FLOAT32
+                          : TinyImageFormat_IsSigned(src->format) ? GIC_SRC_SNORM8
+                                                                  : GIC_SRC_UNORM8;
+    const size_t texel_bytes = st == GIC_SRC_FLOAT32 ? 4 : 1;
     Image_ImageHeader const *dst = Image_CreateNoClear(src->width, src->height, 1, src->slices, dst_fmt);
     if (!dst) return nullptr;
     const uint32_t bx = (src->width + 3) / 4, by = (src->height + 3) / 4;
-    const size_t pitch = (size_t)src->width * ch;
+    const size_t pitch = (size_t)src->width * ch * texel_bytes;
     const size_t src_bytes = pitch * src->height * src->slices;
     const size_t bb = gic_block_bytes(fmt);
     const size_t dst_bytes = (size_t)bx * by * src->slices * bb;
@@ -384,8 +467,8 @@ static Image_ImageHeader const *encode_host_image(Image_ImageHeader const *src, 
         uint8_t *slice_dst = (uint8_t *)s.dst + (size_t)bx * by * bb * w;
         for (uint32_t y0 = 0; ok && y0 < by; y0 += chunk) {
             const uint32_t n = (by - y0) < chunk ? (by - y0) : chunk;
-            ok = gic_hip_encode_rows(fmt, slice_src, src->width, src->height, 1, ch, pitch, y0, n, &o,
-                                     slice_dst + (size_t)y0 * bx * bb, nullptr, s.stream) == GIC_OK;
+            ok = gic_hip_encode_rows_src(fmt, st, slice_src, src->width, src->height, 1, ch, pitch, y0, n, &o,
+                                         slice_dst + (size_t)y0 * bx * bb, nullptr, s.stream) == GIC_OK;
             if (ok && cb) {
                 ok = hipStreamSynchronize(s.stream) == hipSuccess;
                 for (uint32_t y = y0; ok && y < y0 + n; ++y) {

@@ -214,6 +214,90 @@ __device__ __forceinline__ void refine_channels(float cur[3][2], const Col &u, i
     }
 }
 
+// Refine3D, amd_bcx_body.cpp:808-932 (b3DRefinement): the joint jitter of all
+// six endpoint coordinates on the 565 grid, G outermost, then B, then R, each
+// endpoint pair over [-steps, steps] (steps <= 8); the error of a ramp is
+// accumulated channel by channel in the reference's association (G, + B, + R).
+// Arrays past the block's colours hold count-0 entries (add +0).
+template <int N, class Col>
+__device__ void refine_3d(float cur[3][2], const Col &u, int steps)
+{
+    const float wr = 0.3086f, wg = 0.6094f, wb = 0.0820f;
+    float base[3][2], in[3][2], wk[3][2], r[3][4];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) base[ch][e] = in[ch][e] = cur[ch][e];
+    bool flat = expand_grid(wk, in);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) chan_ramp<N>(r[ch], wk[ch]);
+    float best = ramp_fit_error<N>(u, r, flat);
+    if (best == 0.f || !steps) return;
+    const int lo = -(int)minr((float)steps, 8.f), hi = (int)minr((float)steps, 8.f);
+    const float fg = (float)(1 << (8 - chan_bits(CH_G))), fb = (float)(1 << (8 - chan_bits(CH_B))),
+                fr = (float)(1 << (8 - chan_bits(CH_R)));
+    float eg[N][16], egb[N][16];
+    for (int g0 = lo; g0 <= hi; ++g0) {
+        in[CH_G][0] = minr(maxr(base[CH_G][0] + (float)g0 * fg, 0.f), 255.f);
+        for (int g1 = lo; g1 <= hi; ++g1) {
+            in[CH_G][1] = minr(maxr(base[CH_G][1] + (float)g1 * fg, 0.f), 255.f);
+            expand_grid(wk, in);
+            chan_ramp<N>(r[CH_G], wk[CH_G]);
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+#pragma unroll
+                for (int k = 0; k < N; ++k) {
+                    const float d = r[CH_G][k] - u.c(i, CH_G);
+                    eg[k][i] = d * d * wg;
+                }
+            for (int b0 = lo; b0 <= hi; ++b0) {
+                in[CH_B][0] = minr(maxr(base[CH_B][0] + (float)b0 * fb, 0.f), 255.f);
+                for (int b1 = lo; b1 <= hi; ++b1) {
+                    in[CH_B][1] = minr(maxr(base[CH_B][1] + (float)b1 * fb, 0.f), 255.f);
+                    expand_grid(wk, in);
+                    chan_ramp<N>(r[CH_B], wk[CH_B]);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+#pragma unroll
+                        for (int k = 0; k < N; ++k) {
+                            const float d = r[CH_B][k] - u.c(i, CH_B);
+                            egb[k][i] = eg[k][i] + d * d * wb;
+                        }
+                    for (int r0 = lo; r0 <= hi; ++r0) {
+                        in[CH_R][0] = minr(maxr(base[CH_R][0] + (float)r0 * fr, 0.f), 255.f);
+                        for (int r1 = lo; r1 <= hi; ++r1) {
+                            in[CH_R][1] = minr(maxr(base[CH_R][1] + (float)r1 * fr, 0.f), 255.f);
+                            flat = expand_grid(wk, in);
+                            chan_ramp<N>(r[CH_R], wk[CH_R]);
+                            const int nr = flat ? 1 : N;
+                            float mse = 0.f;
+#pragma unroll
+                            for (int i = 0; i < 16; ++i) {
+                                float m = 10000000.f;
+#pragma unroll
+                                for (int k = 0; k < N; ++k) {
+                                    const float d = r[CH_R][k] - u.c(i, CH_R);
+                                    const float e = egb[k][i] + d * d * wr;
+                                    m = (k < nr) ? minr(m, e) : m;
+                                }
+                                mse += m * u.rpt(i);
+                            }
+                            if (mse < best) {
+                                best = mse;
+#pragma unroll
+                                for (int ch = 0; ch < 3; ++ch) {
+                                    cur[ch][0] = in[ch][0];
+                                    cur[ch][1] = in[ch][1];
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
 // RampSrchW, amd_bcx_body.cpp:398-435, over entries [I0, I1) continuing the
 // running sum `error`.  Entries past n have prem = perr = 0 and prj = 0, so
 // they add +0.  (prj - hi >= 0 is prj >= hi and del <= 0 is prj <= lo for
@@ -348,7 +432,7 @@ __device__ __forceinline__ float last_colour(const Col &u, int j)
 }
 
 // CompressRGBBlockX, amd_bcx_body.cpp:937-1203
-template <int N, class Col>
+template <int N, bool R3D, class Col>
 __device__ __forceinline__ void fit_endpoints(float result[3][2], const Col &u, int steps)
 {
     float rc[3][2];
@@ -484,7 +568,10 @@ __device__ __forceinline__ void fit_endpoints(float result[3][2], const Col &u, 
             for (int j = 0; j < 3; ++j) rc[j][k] = (pos_g[k] * dir_g[j] + mid[j]) * 255.f;
     }
     snap_grid(result, rc);
-    refine_channels<N>(result, u, steps);
+    if (R3D)
+        refine_3d<N>(result, u, steps);
+    else
+        refine_channels<N>(result, u, steps);
 }
 
 // Leaders and ranks of the kept texels' colour keys: a kept texel leads its
@@ -681,7 +768,7 @@ __device__ __forceinline__ uint32_t final_indices(const Tex &t, const uint8_t ep
 
 // CompRGBABlock, amd_bcx_body.cpp:1209-1297.  Returns the float error (FLT_MAX
 // for a 4-colour ramp over transparent texels).
-template <int N, class Col, class Tex>
+template <int N, bool R3D = false, class Col, class Tex>
 __device__ __forceinline__ float comp_rgba(const Tex &t, int steps, bool use_alpha, uint8_t ep[3][2], uint32_t &ibits,
                                            const Col &u, int kept)
 {
@@ -696,7 +783,7 @@ __device__ __forceinline__ float comp_rgba(const Tex &t, int steps, bool use_alp
     }
     if (kept != 16 && use_alpha && !(N & 1)) return 3.402823466e+38f;
     float res[3][2];
-    fit_endpoints<N>(res, u, steps);
+    fit_endpoints<N, R3D>(res, u, steps);
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
         ep[ch][0] = (uint8_t)res[ch][0];
@@ -708,14 +795,14 @@ __device__ __forceinline__ float comp_rgba(const Tex &t, int steps, bool use_alp
 }
 
 // Image_CompressAMDBC1Block, amd_bcx_helpers.cpp:51-105
-template <class Col, class Tex>
+template <bool R3D, class Col, class Tex>
 __device__ __forceinline__ uint2 encode_bc1(const Col &u, int kept, const Tex &t, int steps, bool use_alpha)
 {
     uint8_t ep3[3][2], ep4[3][2];
     uint32_t i3 = 0, i4 = 0;
-    const double e3 = comp_rgba<3>(t, steps, use_alpha, ep3, i3, u, kept);
+    const double e3 = comp_rgba<3, R3D>(t, steps, use_alpha, ep3, i3, u, kept);
     double e4 = 3.402823466e+38;
-    if (!(e3 == 0.0)) e4 = comp_rgba<4>(t, steps, use_alpha, ep4, i4, u, kept);
+    if (!(e3 == 0.0)) e4 = comp_rgba<4, R3D>(t, steps, use_alpha, ep4, i4, u, kept);
     const bool m4 = !(e3 <= e4);
     uint8_t ep[3][2];
 #pragma unroll
@@ -736,6 +823,7 @@ __device__ __forceinline__ uint2 encode_bc1(const Col &u, int kept, const Tex &t
     return out;
 }
 
+template <bool R3D>
 __device__ __forceinline__ uint2 encode_bc1_u8(const uint32_t px[16], int steps, bool use_alpha, uint32_t thr_keep,
                                                uint32_t thr_final, const volatile float *lut)
 {
@@ -744,9 +832,10 @@ __device__ __forceinline__ uint2 encode_bc1_u8(const uint32_t px[16], int steps,
     int kept;
     unique_colours(u, px, use_alpha, thr_keep, kept);
     const TexB t{px, thr_final};
-    return encode_bc1(u, kept, t, steps, use_alpha);
+    return encode_bc1<R3D>(u, kept, t, steps, use_alpha);
 }
 
+template <bool R3D>
 __device__ __forceinline__ uint2 encode_bc1_f32(const float in[64], int steps, float thr01)
 {
     const bool use_alpha = thr01 > 0.0f;
@@ -754,7 +843,7 @@ __device__ __forceinline__ uint2 encode_bc1_f32(const float in[64], int steps, f
     int kept;
     unique_colours(u, in, use_alpha, thr01, kept);
     const TexF t{in, thr01 * 255.f};
-    return encode_bc1(u, kept, t, steps, use_alpha);
+    return encode_bc1<R3D>(u, kept, t, steps, use_alpha);
 }
 
 // --------------------------------------------------------- BC2 / BC3 ---
@@ -768,12 +857,12 @@ __device__ __forceinline__ uint2 encode_bc1_f32(const float in[64], int steps, f
 // reference's own 4-colour CompRGBABlock fit with alpha ignored (the BC1 path's
 // second candidate, amd_bcx_helpers.cpp:77-88), packed with c0 > c1 as
 // :164-171 (BC2/BC3 colour blocks are always 4-colour).
-template <class Col, class Tex>
+template <bool R3D, class Col, class Tex>
 __device__ __forceinline__ uint2 encode_rgb4(const Col &u, int kept, const Tex &t, int steps)
 {
     uint8_t ep[3][2];
     uint32_t ib = 0;
-    comp_rgba<4>(t, steps, false, ep, ib, u, kept);
+    comp_rgba<4, R3D>(t, steps, false, ep, ib, u, kept);
     const unsigned c0 = ((unsigned)(ep[CH_R][0] >> 3) << 11) | ((unsigned)(ep[CH_G][0] >> 2) << 5) |
                         (unsigned)(ep[CH_B][0] >> 3);
     const unsigned c1 = ((unsigned)(ep[CH_R][1] >> 3) << 11) | ((unsigned)(ep[CH_G][1] >> 2) << 5) |
@@ -1046,6 +1135,7 @@ struct Bc1Params {
     uint32_t thr_keep, thr_final;   // alpha-byte forms of the two threshold tests
 };
 
+template <bool R3D>
 __global__ void __launch_bounds__(256, 2) bc1_image_kernel(Geometry g, Bc1Params p, uint2 *__restrict__ dst)
 {
     __shared__ float lut[256];   // byte -> v / 255.0f
@@ -1057,7 +1147,7 @@ __global__ void __launch_bounds__(256, 2) bc1_image_kernel(Geometry g, Bc1Params
     block_coords(g, id, slice, by, bx);
     uint32_t px[16];
     load_block_u8(g, slice, by, bx, p.force_alpha_one != 0, px);
-    dst[id] = bcx::encode_bc1_u8(px, p.steps, p.alpha_threshold > 0.0f, p.thr_keep, p.thr_final, lut);
+    dst[id] = bcx::encode_bc1_u8<R3D>(px, p.steps, p.alpha_threshold > 0.0f, p.thr_keep, p.thr_final, lut);
 }
 
 // BC2 / BC3 (amd_bc2_compressor.cpp:36-50, amd_bc3_compressor.cpp:36-50): alpha
@@ -1065,6 +1155,7 @@ __global__ void __launch_bounds__(256, 2) bc1_image_kernel(Geometry g, Bc1Params
 // Image_CompressAMDAlphaSingleModeBlock) then the 4-colour RGB half, one lane
 // per block.  Alpha is the source's (1.0 without an alpha channel, as
 // ReadNxNSplitBlockF's forceAlphaTo1).
+template <bool R3D>
 __global__ void __launch_bounds__(256, 2) bc23_image_kernel(Geometry g, int fmt, Bc1Params p, uint4 *__restrict__ dst)
 {
     __shared__ float lut[256];   // byte -> v / 255.0f
@@ -1091,7 +1182,7 @@ __global__ void __launch_bounds__(256, 2) bc23_image_kernel(Geometry g, int fmt,
     int kept;
     bcx::unique_colours(u, px, false, 0u, kept);
     const bcx::TexB t{px, 0u};
-    const uint2 c = bcx::encode_rgb4(u, kept, t, p.steps);
+    const uint2 c = bcx::encode_rgb4<R3D>(u, kept, t, p.steps);
     dst[id] = make_uint4(a.x, a.y, c.x, c.y);
 }
 
@@ -1120,6 +1211,7 @@ __global__ void __launch_bounds__(256) bc45_image_kernel(Geometry g, int fmt, in
     }
 }
 
+template <bool R3D>
 __global__ void __launch_bounds__(256) bc1_blocks_kernel(const float *__restrict__ blocks, uint32_t n, Bc1Params p,
                                                          uint2 *__restrict__ dst)
 {
@@ -1128,7 +1220,7 @@ __global__ void __launch_bounds__(256) bc1_blocks_kernel(const float *__restrict
     float blk[64];
 #pragma unroll
     for (int i = 0; i < 64; ++i) blk[i] = blocks[(size_t)id * 64 + i];
-    dst[id] = bcx::encode_bc1_f32(blk, p.steps, p.alpha_threshold);
+    dst[id] = bcx::encode_bc1_f32<R3D>(blk, p.steps, p.alpha_threshold);
 }
 
 __global__ void __launch_bounds__(256) bc4_blocks_kernel(const float *__restrict__ blocks, uint32_t n,
@@ -1142,6 +1234,7 @@ __global__ void __launch_bounds__(256) bc4_blocks_kernel(const float *__restrict
     dst[id] = bcx::encode_bc4(v);
 }
 
+template <bool R3D>
 __global__ void __launch_bounds__(256) bc23_blocks_kernel(const float *__restrict__ blocks, uint32_t n, int fmt,
                                                           Bc1Params p, uint4 *__restrict__ dst)
 {
@@ -1163,8 +1256,74 @@ __global__ void __launch_bounds__(256) bc23_blocks_kernel(const float *__restric
     int kept;
     bcx::unique_colours(u, blk, false, 0.f, kept);
     const bcx::TexF t{blk, 0.f};
-    const uint2 c = bcx::encode_rgb4(u, kept, t, p.steps);
+    const uint2 c = bcx::encode_rgb4<R3D>(u, kept, t, p.steps);
     dst[id] = make_uint4(a.x, a.y, c.x, c.y);
+}
+
+// ------------------------------------------------- non-UNORM8 sources ---
+
+// Gather blocks [first, first + n) of a launch geometry as RGBA float blocks
+// (16 texels x 4, texel-major), the float texels Image_GetPixelAtF returns
+// (ReadNxNBlockF, block_utils.cpp:7-41, with its edge clamp).  kind 1: SNORM8,
+// v -> max(v / 127.0f, -1.0f); kind 2: FLOAT32 as stored.  Channels past the
+// source's read 0, alpha 1 (tiny_imageformat's decode is un-vendored, SURVEY.md
+// 8(c): these conversions are this library's, parity against the reference
+// unpinned).  The per-texel loads are scattered; this is a format-conversion
+// pass, the encoders behind it dominate.
+__global__ void __launch_bounds__(256) gather_f32_kernel(Geometry g, int kind, int force_alpha_one, uint32_t first,
+                                                         uint32_t n, float *__restrict__ out)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    uint32_t slice, by, bx;
+    block_coords(g, first + k, slice, by, bx);
+    const uint8_t *img = g.src + (size_t)slice * g.row_pitch * g.height;
+    float *o = out + (size_t)k * 64;
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+        uint32_t sy = by * 4 + y;
+        sy = sy >= g.height ? g.height - 1 : sy;
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+            uint32_t sx = bx * 4 + x;
+            sx = sx >= g.width ? g.width - 1 : sx;
+            float v[4] = {0.f, 0.f, 0.f, 1.f};
+            if (kind == 1) {
+                const int8_t *p = reinterpret_cast<const int8_t *>(img + (size_t)sy * g.row_pitch + (size_t)sx * g.channels);
+                for (uint32_t c = 0; c < g.channels && c < 4; ++c) v[c] = maxr((float)p[c] / 127.0f, -1.0f);
+            } else {
+                const float *p = reinterpret_cast<const float *>(img + (size_t)sy * g.row_pitch) + (size_t)sx * g.channels;
+                for (uint32_t c = 0; c < g.channels && c < 4; ++c) v[c] = p[c];
+            }
+            if (force_alpha_one) v[3] = 1.f;
+            float *t = o + (y * 4 + x) * 4;
+            t[0] = v[0];
+            t[1] = v[1];
+            t[2] = v[2];
+            t[3] = v[3];
+        }
+    }
+}
+
+// BC4 (channel `channel`) or BC5 (channels 0, 1) from RGBA float blocks
+__global__ void __launch_bounds__(256) bc45_rgba_blocks_kernel(const float *__restrict__ blocks, uint32_t n, int fmt,
+                                                               int channel, uint64_t *__restrict__ dst)
+{
+    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= n) return;
+    float v[16];
+    if (fmt == 4) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = blocks[(size_t)id * 64 + i * 4 + channel];
+        dst[id] = bcx::encode_bc4(v);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = blocks[(size_t)id * 64 + i * 4];
+        dst[2 * (size_t)id] = bcx::encode_bc4(v);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = blocks[(size_t)id * 64 + i * 4 + 1];
+        dst[2 * (size_t)id + 1] = bcx::encode_bc4(v);
+    }
 }
 
 // ------------------------------------------------------------- decode ---
@@ -1289,6 +1448,21 @@ __global__ void __launch_bounds__(256) bcx_decode_kernel(const uint8_t *__restri
 
 // ------------------------------------------------------------ launchers ---
 
+hipError_t launch_gather_f32(const Geometry &g, int kind, int force_alpha_one, uint32_t first, uint32_t n, float *out,
+                             hipStream_t s)
+{
+    const uint32_t wg = 256, grid = (n + wg - 1) / wg;
+    hipLaunchKernelGGL(gather_f32_kernel, dim3(grid), dim3(wg), 0, s, g, kind, force_alpha_one, first, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_bc45_rgba_blocks(const float *blocks, uint32_t n, int fmt, int channel, void *dst, hipStream_t s)
+{
+    const uint32_t wg = 256, grid = (n + wg - 1) / wg;
+    hipLaunchKernelGGL(bc45_rgba_blocks_kernel, dim3(grid), dim3(wg), 0, s, blocks, n, fmt, channel, (uint64_t *)dst);
+    return hipGetLastError();
+}
+
 hipError_t launch_bcx_decode(const uint8_t *blocks, int fmt, uint32_t width, uint32_t height, uint32_t slices,
                              uint8_t *out, size_t row_pitch, hipStream_t s)
 {
@@ -1311,7 +1485,7 @@ static uint32_t first_byte(F pass)
     return 256;
 }
 
-hipError_t launch_bc1_image(const Geometry &g, float thr, int steps, int force_alpha_one, void *dst,
+hipError_t launch_bc1_image(const Geometry &g, float thr, int steps, int force_alpha_one, int r3d, void *dst,
                             hipStream_t s)
 {
     // CompRGBABlock keeps a texel when a / 255.0f >= thr; ClstrIntnl marks it
@@ -1323,23 +1497,33 @@ hipError_t launch_bc1_image(const Geometry &g, float thr, int steps, int force_a
     const uint32_t fin = first_byte([&](uint32_t a) { return (float)a >= t255; });
     const Bc1Params p{thr, steps, force_alpha_one, keep, fin};
     const uint32_t wg = 256, grid = (g.total + wg - 1) / wg;
-    hipLaunchKernelGGL(bc1_image_kernel, dim3(grid), dim3(wg), 0, s, g, p, (uint2 *)dst);
+    if (r3d)
+        hipLaunchKernelGGL(bc1_image_kernel<true>, dim3(grid), dim3(wg), 0, s, g, p, (uint2 *)dst);
+    else
+        hipLaunchKernelGGL(bc1_image_kernel<false>, dim3(grid), dim3(wg), 0, s, g, p, (uint2 *)dst);
     return hipGetLastError();
 }
 
-hipError_t launch_bc23_image(const Geometry &g, int fmt, int steps, int force_alpha_one, void *dst, hipStream_t s)
+hipError_t launch_bc23_image(const Geometry &g, int fmt, int steps, int force_alpha_one, int r3d, void *dst,
+                             hipStream_t s)
 {
     const Bc1Params p{0.f, steps, force_alpha_one, 0u, 0u};
     const uint32_t wg = 256, grid = (g.total + wg - 1) / wg;
-    hipLaunchKernelGGL(bc23_image_kernel, dim3(grid), dim3(wg), 0, s, g, fmt, p, (uint4 *)dst);
+    if (r3d)
+        hipLaunchKernelGGL(bc23_image_kernel<true>, dim3(grid), dim3(wg), 0, s, g, fmt, p, (uint4 *)dst);
+    else
+        hipLaunchKernelGGL(bc23_image_kernel<false>, dim3(grid), dim3(wg), 0, s, g, fmt, p, (uint4 *)dst);
     return hipGetLastError();
 }
 
-hipError_t launch_bc23_blocks(const float *blocks, uint32_t n, int fmt, int steps, void *dst, hipStream_t s)
+hipError_t launch_bc23_blocks(const float *blocks, uint32_t n, int fmt, int steps, int r3d, void *dst, hipStream_t s)
 {
     const Bc1Params p{0.f, steps, 0, 0u, 0u};
     const uint32_t wg = 256, grid = (n + wg - 1) / wg;
-    hipLaunchKernelGGL(bc23_blocks_kernel, dim3(grid), dim3(wg), 0, s, blocks, n, fmt, p, (uint4 *)dst);
+    if (r3d)
+        hipLaunchKernelGGL(bc23_blocks_kernel<true>, dim3(grid), dim3(wg), 0, s, blocks, n, fmt, p, (uint4 *)dst);
+    else
+        hipLaunchKernelGGL(bc23_blocks_kernel<false>, dim3(grid), dim3(wg), 0, s, blocks, n, fmt, p, (uint4 *)dst);
     return hipGetLastError();
 }
 
@@ -1350,11 +1534,14 @@ hipError_t launch_bc45_image(const Geometry &g, int fmt, int channel, void *dst,
     return hipGetLastError();
 }
 
-hipError_t launch_bc1_blocks(const float *blocks, uint32_t n, float thr, int steps, void *dst, hipStream_t s)
+hipError_t launch_bc1_blocks(const float *blocks, uint32_t n, float thr, int steps, int r3d, void *dst, hipStream_t s)
 {
     const Bc1Params p{thr, steps, 0, 0u, 0u};
     const uint32_t wg = 256, grid = (n + wg - 1) / wg;
-    hipLaunchKernelGGL(bc1_blocks_kernel, dim3(grid), dim3(wg), 0, s, blocks, n, p, (uint2 *)dst);
+    if (r3d)
+        hipLaunchKernelGGL(bc1_blocks_kernel<true>, dim3(grid), dim3(wg), 0, s, blocks, n, p, (uint2 *)dst);
+    else
+        hipLaunchKernelGGL(bc1_blocks_kernel<false>, dim3(grid), dim3(wg), 0, s, blocks, n, p, (uint2 *)dst);
     return hipGetLastError();
 }
 

@@ -36,6 +36,13 @@ typedef enum gic_format {
     GIC_FMT_BC7 = 7  /* BC7BlockEncoder::CompressBlock (amd_bc7_body.cpp:1289) */
 } gic_format;
 
+/* Texel encodings of a source image (what Image_GetPixelAtF decodes). */
+typedef enum gic_source {
+    GIC_SRC_UNORM8 = 0, /* bytes, v / 255.0f (R8..R8G8B8A8 UNORM and sRGB) */
+    GIC_SRC_SNORM8 = 1, /* signed bytes, max(v / 127.0f, -1.0f) (R8_SNORM, R8G8_SNORM) */
+    GIC_SRC_FLOAT32 = 2 /* 32-bit floats as stored (R32G32B32A32_SFLOAT) */
+} gic_source;
+
 /* Options; gic_default_options() gives the reference defaults
  * (Image_CompressDefaultAmdOptions, amd_bcx_helpers.cpp:23-31; BC1 options,
  * amd_bc1_compressor.cpp:21-27; BC7 wrapper arguments, amd_bc7_compressor.cpp:58-65). */
@@ -43,7 +50,7 @@ typedef struct gic_options {
     uint32_t struct_size;        /* sizeof(gic_options) */
     float bc1_alpha_threshold;   /* 0..1; <= 0 disables punch-through (default 128/255) */
     uint8_t refinement_steps;    /* AMD RefinementSteps, 0..8 (default 1) */
-    uint8_t b3d_refinement;      /* must be 0 (Refine3D not implemented) */
+    uint8_t b3d_refinement;      /* AMD b3DRefinement: Refine3D's joint 6-D endpoint jitter (BC1/BC2/BC3) */
     uint8_t adaptive_weights;    /* must be 0 (reference path is UB: block_utils.cpp:201-203) */
     uint8_t bc4_channel;         /* source channel for BC4 (reference reads 1: amd_bc4_compressor.cpp:34) */
     uint8_t bc7_mode_mask;       /* default 0xFF (0 means 0xCF, amd_bc7_body.hpp:103-106) */
@@ -81,6 +88,16 @@ int gic_hip_encode_rows(gic_format fmt, const uint8_t *d_src, uint32_t width, ui
                         uint32_t slices, uint32_t channels, size_t row_pitch,
                         uint32_t first_block_row, uint32_t num_block_rows, const gic_options *opt,
                         uint8_t *d_dst, double *d_block_err, void *stream);
+
+/* gic_hip_encode_rows for any gic_source: UNORM8 runs the byte kernels
+ * directly; SNORM8 / FLOAT32 texels are gathered into float blocks on the
+ * device (stream-ordered scratch of <= 256 MiB) and encoded by the block-level
+ * kernels (the reference's float block path: every format accepts any texels
+ * Image_GetPixelAtF returns, block_utils.cpp:24-26).  row_pitch in bytes. */
+int gic_hip_encode_rows_src(gic_format fmt, gic_source src_type, const void *d_src, uint32_t width,
+                            uint32_t height, uint32_t slices, uint32_t channels, size_t row_pitch,
+                            uint32_t first_block_row, uint32_t num_block_rows, const gic_options *opt,
+                            uint8_t *d_dst, double *d_block_err, void *stream);
 
 /* Block-level batch: n blocks of 16 texels, float in [0,1].
  *   BC1/BC2/BC3/BC7: d_blocks holds n x 64 floats (RGBA per texel, texel-major).

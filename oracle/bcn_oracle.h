@@ -27,12 +27,16 @@ extern "C" {
 void orc_bc1_block(const float in[64], int refinement_steps,
                    float alpha_threshold01, uint8_t out[8]);
 
+/* the same with the AMD b3DRefinement option (Refine3D, amd_bcx_body.cpp:808-932) */
+void orc_bc1_block_ex(const float in[64], int refinement_steps, float alpha_threshold01, int b3d,
+                      uint8_t out[8]);
+
 /* Image_CompressAMDAlphaSingleModeBlock (amd_bcx_helpers.cpp:125-140). */
 void orc_bc4_block(const float in[16], uint8_t out[8]);
 
 /* BC2/BC3 halves: the 4-colour RGB block (alpha ignored; the reference's
  * CompRGBBlock is UB, see orc_bcx.c) and the explicit 4-bit alpha block. */
-void orc_rgb4_block(const float in[64], int refinement_steps, uint8_t out[8]);
+void orc_rgb4_block(const float in[64], int refinement_steps, int b3d, uint8_t out[8]);
 void orc_explicit_alpha_block(const float in[16], uint8_t out[8]);
 
 /* BC7BlockEncoder::CompressBlock (amd_bc7_body.cpp:1289-1465) with the

@@ -356,9 +356,82 @@ static void refine_channels(float out[3][2], float in[3][2], float blk[16][4],
             out[ch][e] = cur[ch][e];
 }
 
+/* Refine3D, amd_bcx_body.cpp:808-932 (b3DRefinement): joint jitter of the six
+ * endpoint coordinates, G outermost, then B, then R. */
+static void refine_3d(float out[3][2], float in0[3][2], float blk[16][4], const float rpt[16], int ncol, int n,
+                      const float w[3], int steps)
+{
+    const float wr = w[0], wg = w[1], wb = w[2];
+    float rmp[3][4], inp0[3][2], inp[3][2], wk[3][2];
+    for (int k = 0; k < 2; ++k)
+        for (int j = 0; j < 3; ++j)
+            inp0[j][k] = inp[j][k] = out[j][k] = in0[j][k];
+    int eq = expand_grid(wk, inp);
+    colour_ramp(rmp, wk, n);
+    float best = ramp_fit_error(blk, rpt, rmp, ncol, n, eq, w);
+    if (best == 0.f || !steps)
+        return;
+    const int lo = 0 - (int)fminr((float)steps, 8.f), hi = (int)fminr((float)steps, 8.f);
+    const float fr = (float)(1 << (8 - chan_bits(CH_R))), fg = (float)(1 << (8 - chan_bits(CH_G))),
+                fb = (float)(1 << (8 - chan_bits(CH_B)));
+    for (int g0 = lo; g0 <= hi; g0++) {
+        inp[CH_G][0] = fminr(fmaxr(inp0[CH_G][0] + g0 * fg, 0.f), 255.f);
+        for (int g1 = lo; g1 <= hi; g1++) {
+            inp[CH_G][1] = fminr(fmaxr(inp0[CH_G][1] + g1 * fg, 0.f), 255.f);
+            eq = expand_grid(wk, inp);
+            chan_ramp(rmp[CH_G], wk[CH_G], n);
+            float errg[4][16];
+            for (int i = 0; i < ncol; i++)
+                for (int r = 0; r < n; r++) {
+                    float dg = rmp[CH_G][r] - blk[i][CH_G];
+                    errg[r][i] = dg * dg * wg;
+                }
+            for (int b0 = lo; b0 <= hi; b0++) {
+                inp[CH_B][0] = fminr(fmaxr(inp0[CH_B][0] + b0 * fb, 0.f), 255.f);
+                for (int b1 = lo; b1 <= hi; b1++) {
+                    inp[CH_B][1] = fminr(fmaxr(inp0[CH_B][1] + b1 * fb, 0.f), 255.f);
+                    eq = expand_grid(wk, inp);
+                    chan_ramp(rmp[CH_B], wk[CH_B], n);
+                    float err[4][16];
+                    for (int i = 0; i < ncol; i++)
+                        for (int r = 0; r < n; r++) {
+                            float db = rmp[CH_B][r] - blk[i][CH_B];
+                            err[r][i] = errg[r][i] + db * db * wb;
+                        }
+                    for (int r0 = lo; r0 <= hi; r0++) {
+                        inp[CH_R][0] = fminr(fmaxr(inp0[CH_R][0] + r0 * fr, 0.f), 255.f);
+                        for (int r1 = lo; r1 <= hi; r1++) {
+                            inp[CH_R][1] = fminr(fmaxr(inp0[CH_R][1] + r1 * fr, 0.f), 255.f);
+                            eq = expand_grid(wk, inp);
+                            chan_ramp(rmp[CH_R], wk[CH_R], n);
+                            float mse = 0.f;
+                            const int rl = eq ? 1 : n;
+                            for (int k = 0; k < ncol; k++) {
+                                float m = 10000000.f;
+                                for (int r = 0; r < rl; r++) {
+                                    float d = rmp[CH_R][r] - blk[k][CH_R];
+                                    float e2 = err[r][k] + d * d * wr;
+                                    m = fminr(m, e2);
+                                }
+                                mse += m * rpt[k];
+                            }
+                            if (mse < best) {
+                                best = mse;
+                                for (int k = 0; k < 2; k++)
+                                    for (int j = 0; j < 3; j++)
+                                        out[j][k] = inp[j][k];
+                            }
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
 /* CompressRGBBlockX, amd_bcx_body.cpp:937-1203.  blkin: unique colours x255. */
 static void fit_endpoints(float result[3][2], float blkin[16][4], const float rpt[16],
-                          int nuniq, int n, int steps, const float w[3])
+                          int nuniq, int n, int steps, const float w[3], int b3d)
 {
     float blk[16][4], sh[16][4], dir0[3], mid[3];
     float rc[3][2];
@@ -480,7 +553,10 @@ static void fit_endpoints(float result[3][2], float blkin[16][4], const float rp
     }
     float grid[3][2];
     snap_grid(grid, rc);
-    refine_channels(result, grid, blkin, rpt, nuniq, n, w, steps);
+    if (b3d)
+        refine_3d(result, grid, blkin, rpt, nuniq, n, w, steps);
+    else
+        refine_channels(result, grid, blkin, rpt, nuniq, n, w, steps);
 }
 
 static int rgb_key_less(const float *a, const float *b)
@@ -497,7 +573,7 @@ static int rgb_key_less(const float *a, const float *b)
 /* CompRGBABlock, amd_bcx_body.cpp:1209-1297.  Returns FLT_MAX (as float) when
  * a 4-colour ramp is requested for a block with transparent texels. */
 static float comp_rgba_block(const float *in, uint8_t ep[3][2], uint8_t idx[16], int n,
-                             int steps, const float w[3], int use_alpha, float thr01)
+                             int steps, const float w[3], int use_alpha, float thr01, int b3d)
 {
     float rec[16][4];
     int ncol = 0;
@@ -551,7 +627,7 @@ static float comp_rgba_block(const float *in, uint8_t ep[3][2], uint8_t idx[16],
         for (int j = 0; j < 4; ++j)
             uniq[i][j] = (float)((double)uniq[i][j] * 255.0);
     float res[3][2];
-    fit_endpoints(res, uniq, rpt, nu, n, steps, w);
+    fit_endpoints(res, uniq, rpt, nu, n, steps, w, b3d);
     for (int ch = 0; ch < 3; ++ch)
         for (int e = 0; e < 2; ++e)
             ep[ch][e] = (uint8_t)res[ch][e];
@@ -566,16 +642,21 @@ static float comp_rgba_block(const float *in, uint8_t ep[3][2], uint8_t idx[16],
 }
 
 /* Image_CompressAMDBC1Block, amd_bcx_helpers.cpp:51-105 (non-adaptive
- * weights block_utils.cpp:162-173; b3DRefinement unsupported). */
+ * weights block_utils.cpp:162-173; b3DRefinement -> Refine3D in the _ex form). */
 void orc_bc1_block(const float in[64], int refinement_steps, float alpha_threshold01, uint8_t out8[8])
+{
+    orc_bc1_block_ex(in, refinement_steps, alpha_threshold01, 0, out8);
+}
+
+void orc_bc1_block_ex(const float in[64], int refinement_steps, float alpha_threshold01, int b3d, uint8_t out8[8])
 {
     const float w[3] = {0.3086f, 0.6094f, 0.0820f};
     uint8_t ep[2][3][2], idx[2][16];
     const int use_alpha = alpha_threshold01 > 0.0f;
-    double e3 = comp_rgba_block(in, ep[0], idx[0], 3, refinement_steps, w, use_alpha, alpha_threshold01);
+    double e3 = comp_rgba_block(in, ep[0], idx[0], 3, refinement_steps, w, use_alpha, alpha_threshold01, b3d);
     double e4 = (e3 == 0.0) ? FLT_MAX
                             : comp_rgba_block(in, ep[1], idx[1], 4, refinement_steps, w, use_alpha,
-                                              alpha_threshold01);
+                                              alpha_threshold01, b3d);
     const int m = (e3 <= e4) ? 0 : 1;
     unsigned c0 = ((unsigned)(ep[m][CH_R][0] >> 3) << 11) | ((unsigned)(ep[m][CH_G][0] >> 2) << 5) |
                   (unsigned)(ep[m][CH_B][0] >> 3);
@@ -600,11 +681,11 @@ void orc_bc1_block(const float in[64], int refinement_steps, float alpha_thresho
  * -- packed with c0 > c1 as :164-171.  Parity of this half is unpinned (no
  * reference output exists to pin it); the alpha halves are pinned by the BC4
  * restatement they share. */
-void orc_rgb4_block(const float in[64], int refinement_steps, uint8_t out8[8])
+void orc_rgb4_block(const float in[64], int refinement_steps, int b3d, uint8_t out8[8])
 {
     const float w[3] = {0.3086f, 0.6094f, 0.0820f};
     uint8_t ep[3][2], idx[16];
-    comp_rgba_block(in, ep, idx, 4, refinement_steps, w, 0, 0.f);
+    comp_rgba_block(in, ep, idx, 4, refinement_steps, w, 0, 0.f, b3d);
     unsigned c0 = ((unsigned)(ep[CH_R][0] >> 3) << 11) | ((unsigned)(ep[CH_G][0] >> 2) << 5) |
                   (unsigned)(ep[CH_B][0] >> 3);
     unsigned c1 = ((unsigned)(ep[CH_R][1] >> 3) << 11) | ((unsigned)(ep[CH_G][1] >> 2) << 5) |

@@ -92,7 +92,7 @@ static void encode_row(job_t *j, uint32_t slice, uint32_t brow)
                 orc_bc4_block(ch, o);
             else
                 orc_explicit_alpha_block(ch, o);
-            orc_rgb4_block(blk, 1, o + 8);
+            orc_rgb4_block(blk, 1, 0, o + 8);
             break;
         case 4:
             for (int i = 0; i < 16; ++i) ch[i] = blk[i * 4 + j->bc4_channel];

@@ -43,7 +43,8 @@ def lib() -> ctypes.CDLL:
         _lib.orc_encode_image_bc7_ex.restype = ctypes.c_int
         _lib.orc_bc1_block.argtypes = [vp, ctypes.c_int, ctypes.c_float, vp]
         _lib.orc_bc4_block.argtypes = [vp, vp]
-        _lib.orc_rgb4_block.argtypes = [vp, ctypes.c_int, vp]
+        _lib.orc_rgb4_block.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
+        _lib.orc_bc1_block_ex.argtypes = [vp, ctypes.c_int, ctypes.c_float, ctypes.c_int, vp]
         _lib.orc_explicit_alpha_block.argtypes = [vp, vp]
         _lib.orc_bc7_block.argtypes = [vp, ctypes.c_uint8, ctypes.c_int, ctypes.c_float, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_float, vp]
@@ -104,10 +105,10 @@ def encode_image_bc7(img: np.ndarray, quality: float = 1.0, mode_mask: int = 0xF
     return (out, err) if want_err else out
 
 
-def bc1_block(block: np.ndarray, steps: int = 1, threshold: float = 128 / 255.0) -> bytes:
+def bc1_block(block: np.ndarray, steps: int = 1, threshold: float = 128 / 255.0, b3d: bool = False) -> bytes:
     b = np.ascontiguousarray(block, dtype=np.float32).reshape(64)
     out = np.zeros(8, np.uint8)
-    lib().orc_bc1_block(b.ctypes.data, steps, threshold, out.ctypes.data)
+    lib().orc_bc1_block_ex(b.ctypes.data, steps, threshold, int(b3d), out.ctypes.data)
     return out.tobytes()
 
 
@@ -118,7 +119,7 @@ def bc4_block(values: np.ndarray) -> bytes:
     return out.tobytes()
 
 
-def bc23_block(fmt: int, block: np.ndarray, steps: int = 1) -> bytes:
+def bc23_block(fmt: int, block: np.ndarray, steps: int = 1, b3d: bool = False) -> bytes:
     """BC2 (fmt 2) / BC3 (fmt 3) block from 16 RGBA float texels: alpha half, colour half."""
     b = np.ascontiguousarray(block, dtype=np.float32).reshape(64)
     a = np.ascontiguousarray(b.reshape(16, 4)[:, 3])
@@ -128,7 +129,7 @@ def bc23_block(fmt: int, block: np.ndarray, steps: int = 1) -> bytes:
     else:
         lib().orc_explicit_alpha_block(a.ctypes.data, out.ctypes.data)
     col = np.zeros(8, np.uint8)
-    lib().orc_rgb4_block(b.ctypes.data, steps, col.ctypes.data)
+    lib().orc_rgb4_block(b.ctypes.data, steps, int(b3d), col.ctypes.data)
     out[8:] = col
     return out.tobytes()
 

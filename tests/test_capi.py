@@ -55,7 +55,7 @@ def test_block_bytes_and_argument_checks():
     assert lib.gic_block_bytes(5) == 16 and lib.gic_block_bytes(7) == 16
     # invalid arguments are rejected before any HIP call
     assert lib.gic_hip_encode(1, None, 4, 4, 1, 4, 16, None, None, None, None) == gic.GIC_EINVAL
-    o = gic.Options(b3d_refinement=True).to_c()
+    o = gic.Options(adaptive_weights=True).to_c()
     assert lib.gic_hip_encode(1, 16, 4, 4, 1, 4, 16, ctypes.byref(o), 16, None, None) == gic.GIC_EUNSUP
 
 

@@ -131,6 +131,34 @@ def test_bc1_refinement_steps_option(gpu):
         assert np.array_equal(out, np.frombuffer(b"".join(blocks), np.uint8).reshape(-1, 8)), steps
 
 
+@pytest.mark.parametrize("steps", [1, 2])
+def test_bc1_b3d_refinement_option(gpu, steps):
+    """AMD b3DRefinement (Refine3D's joint 6-D jitter, amd_bcx_body.cpp:808-932):
+    BC1 image path on G1 and the BC3 colour half / float block path on noise."""
+    import torch
+    img = synth.g1(32, 32) if steps == 1 else synth.g1(16, 16)
+    n = (img.shape[0] // 4) * (img.shape[1] // 4)
+    out = gpu_encode(gic.FMT_BC1, img, gic.Options(refinement_steps=steps, b3d_refinement=True))
+    side = img.shape[1] // 4
+    blocks = [oracle_lib.bc1_block(_block_f32(img, bx, by), steps=steps, b3d=True)
+              for by in range(img.shape[0] // 4) for bx in range(side)]
+    assert np.array_equal(out, np.frombuffer(b"".join(blocks), np.uint8).reshape(-1, 8))
+    assert n == len(blocks)
+    rng = np.random.default_rng(40 + steps)
+    fb = rng.random((32, 16, 4), dtype=np.float32)
+    fb[::2] = np.round(fb[::2] * 255) / np.float32(255.0)
+    t = torch.from_numpy(fb.reshape(-1, 64)).cuda()
+    for fmt in (gic.FMT_BC1, gic.FMT_BC3):
+        dst = torch.zeros(32 * gic.block_bytes(fmt), dtype=torch.uint8, device="cuda")
+        gic.encode_blocks_f32(fmt, t, dst, gic.Options(refinement_steps=steps, b3d_refinement=True))
+        torch.cuda.synchronize()
+        got = dst.cpu().numpy().reshape(32, -1)
+        for i, b in enumerate(fb):
+            ref = oracle_lib.bc1_block(b, steps=steps, b3d=True) if fmt == gic.FMT_BC1 else \
+                oracle_lib.bc23_block(fmt, b, steps=steps, b3d=True)
+            assert got[i].tobytes() == ref, (fmt, i)
+
+
 def _block_f32(img, bx, by):
     return img[by * 4:by * 4 + 4, bx * 4:bx * 4 + 4].reshape(16, 4).astype(np.float32) / np.float32(255.0)
 
@@ -247,3 +275,96 @@ def test_bc3_full_8k_bit_exact(gpu):
     out = gpu_encode(3, img)
     ref = oracle_lib.encode_image(3, img)
     assert np.array_equal(out, ref), _mismatch_report(out, ref)
+
+
+def _float_blocks(tex, w, h):
+    """(H, W, 4) float texels -> (by*bx, 16, 4) blocks with ReadNxNBlockF's edge clamp."""
+    bx, by = (w + 3) // 4, (h + 3) // 4
+    ys = np.minimum(np.arange(by * 4), h - 1)
+    xs = np.minimum(np.arange(bx * 4), w - 1)
+    t = tex[ys][:, xs]
+    return t.reshape(by, 4, bx, 4, 4).transpose(0, 2, 1, 3, 4).reshape(-1, 16, 4).astype(np.float32)
+
+
+@pytest.mark.parametrize("fmt", [4, 5])
+def test_snorm8_sources_bc45(gpu, fmt):
+    """R8_SNORM / R8G8_SNORM sources (amd_bc4/bc5_compressor.cpp:16-19): texels
+    max(v / 127.0f, -1.0f), encoded like the reference's float block path."""
+    import torch
+    w, h, c = 30, 22, (1 if fmt == 4 else 2)
+    rng = np.random.default_rng(fmt)
+    img = rng.integers(-128, 128, (h, w, c), dtype=np.int8)
+    img[:8] = np.clip(np.arange(w) * 9 - 128, -128, 127).astype(np.int8)[None, :, None]   # ramps
+    src = torch.from_numpy(img.copy()).cuda()
+    bx, by = (w + 3) // 4, (h + 3) // 4
+    dst = torch.zeros(bx * by * gic.block_bytes(fmt), dtype=torch.uint8, device="cuda")
+    gic.encode_device_src(fmt, gic.SRC_SNORM8, src, w, h, 1, c, dst, gic.Options(bc4_channel=0))
+    torch.cuda.synchronize()
+    got = dst.cpu().numpy().reshape(-1, gic.block_bytes(fmt))
+    tex = np.zeros((h, w, 4), np.float32)
+    tex[..., 3] = 1.0
+    tex[..., :c] = np.maximum(img.astype(np.float32) / np.float32(127.0), np.float32(-1.0))
+    blocks = _float_blocks(tex, w, h)
+    for i, b in enumerate(blocks):
+        ref = oracle_lib.bc4_block(b[:, 0])
+        if fmt == 5:
+            ref += oracle_lib.bc4_block(b[:, 1])
+        assert got[i].tobytes() == ref, i
+
+
+@pytest.mark.parametrize("fmt", [1, 3, 7])
+def test_float32_sources(gpu, fmt):
+    """R32G32B32A32_SFLOAT sources: float texels as stored through the float
+    block encoders (BC1/BC3 with values outside [0, 1] too; BC7 inside it:
+    the reference indexes its 256-entry single-point tables with floor/ceil
+    of the texel, amd_shake.cpp:627-635, out of bounds for other values)."""
+    import torch
+    w, h = 21, 13 if fmt == 7 else 26
+    rng = np.random.default_rng(10 + fmt)
+    tex = rng.random((h, w, 4), dtype=np.float32)
+    if fmt != 7:
+        tex = tex * np.float32(1.2) - np.float32(0.1)
+    tex[:, :, 3] = np.where(rng.random((h, w)) < 0.8, np.float32(1.0), tex[:, :, 3])
+    src = torch.from_numpy(tex.copy()).cuda()
+    bx, by = (w + 3) // 4, (h + 3) // 4
+    dst = torch.zeros(bx * by * gic.block_bytes(fmt), dtype=torch.uint8, device="cuda")
+    gic.encode_device_src(fmt, gic.SRC_FLOAT32, src, w, h, 1, 4, dst)
+    torch.cuda.synchronize()
+    got = dst.cpu().numpy().reshape(-1, gic.block_bytes(fmt))
+    for i, b in enumerate(_float_blocks(tex, w, h)):
+        if fmt == 1:
+            ref = oracle_lib.bc1_block(b)
+        elif fmt == 3:
+            ref = oracle_lib.bc23_block(3, b)
+        else:
+            ref = oracle_lib.bc7_block(b)[0]
+        assert got[i].tobytes() == ref, i
+
+
+def test_host_api_snorm_source_gives_snorm_destination(gpu):
+    """Image_CompressAMDBC4 on an R8_SNORM image returns a DXBC4_SNORM image
+    (amd_bc4_compressor.cpp:16-19) with the device path's blocks."""
+    import torch
+    lib = gic.library()
+    lib.Image_CreateNoClear.restype = ctypes.c_void_p
+    lib.Image_RawDataPtr.argtypes = [ctypes.c_void_p]
+    lib.Image_RawDataPtr.restype = ctypes.c_void_p
+    lib.Image_Destroy.argtypes = [ctypes.c_void_p]
+    lib.Image_CompressAMDBC4.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.Image_CompressAMDBC4.restype = ctypes.c_void_p
+    rng = np.random.default_rng(3)
+    img = rng.integers(-128, 128, (16, 24, 1), dtype=np.int8)
+    p = lib.Image_CreateNoClear(24, 16, 1, 1, 2)   # R8_SNORM
+    ctypes.memmove(lib.Image_RawDataPtr(p), img.tobytes(), img.nbytes)
+    q = lib.Image_CompressAMDBC4(p, None, None)
+    assert q
+    fmt_field = ctypes.c_int.from_address(q + 24).value
+    assert fmt_field == 15   # TinyImageFormat_DXBC4_SNORM
+    out = np.ctypeslib.as_array(ctypes.cast(lib.Image_RawDataPtr(q), ctypes.POINTER(ctypes.c_uint8)), (192,)).copy()
+    src = torch.from_numpy(img.copy()).cuda()
+    dst = torch.zeros(24 * 8, dtype=torch.uint8, device="cuda")
+    gic.encode_device_src(4, gic.SRC_SNORM8, src, 24, 16, 1, 1, dst)   # channel 1 (Q1): of an R8 source, zeros
+    torch.cuda.synchronize()
+    assert out.tobytes() == dst.cpu().numpy().tobytes()
+    lib.Image_Destroy(q)
+    lib.Image_Destroy(p)
