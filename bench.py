@@ -391,7 +391,9 @@ def batch_workload(args, gic, world, rank, dev):
             "vs_baseline": None, "dtype": "f64+int32", "data": "synthetic",
             "config": {"workload": f"configs[4]: BC7 quality {args.bc7_quality:g} on a batch of {S}x{n}x{n} "
                                    f"RGBA8 G1 slices (seed 0x9E3779B9+s), block rows of every slice split over "
-                                   f"{world} rank(s), RCCL all-gather to rank 0 timed separately",
+                                   f"{world} rank(s), "
+                                   f"{'RCCL' if world == 1 or dist.get_backend() != 'gloo' else 'gloo (rehearsal)'} "
+                                   f"all-gather to rank 0 timed separately",
                        "format": "BC7", "slices": S, "width": n, "global_batch_blocks": total_blocks,
                        "bc7_search": "exact" if args.bc7_shake_ranks == 0 else
                        f"pruned, {args.bc7_shake_ranks} partitions shaken per mode (per-block MSE tolerance)",
