@@ -20,12 +20,14 @@ import os
 from dataclasses import dataclass, replace
 
 __all__ = [
-    "GicError", "Options", "FMT_BC1", "FMT_BC2", "FMT_BC3", "FMT_BC4", "FMT_BC5", "FMT_BC7", "library",
+    "GicError", "Options", "FMT_BC1", "FMT_BC2", "FMT_BC3", "FMT_BC4", "FMT_BC5", "FMT_BC7", "FMT_BC7ENC16",
+    "library", "encode_blocks_u8", "compress_bc7_fast",
     "block_bytes", "blocks_shape", "encode_device", "encode_device_src", "encode_blocks_f32", "decode_device", "compress_bc1", "compress_bc2",
     "compress_bc3", "compress_bc4", "compress_bc5", "compress_bc7", "LIB_PATH",
 ]
 
 FMT_BC1, FMT_BC2, FMT_BC3, FMT_BC4, FMT_BC5, FMT_BC7 = 1, 2, 3, 4, 5, 7
+FMT_BC7ENC16 = 8   # BC7 by bc7enc16, the reference's fast encoder (richgel999_bc7enc16.cpp)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GIC_LIBRARY") or os.path.join(_HERE, "lib", "libgfx_imagecompress_amd.so")
 
@@ -52,6 +54,11 @@ class _COptions(ctypes.Structure):
         ("bc7_quality", ctypes.c_float),
         ("bc7_performance", ctypes.c_float),
         ("bc7_shake_ranks", ctypes.c_uint32),
+        ("bc7enc_perceptual", ctypes.c_uint8),
+        ("bc7enc_uber_level", ctypes.c_uint8),
+        ("bc7enc_max_partitions", ctypes.c_uint8),
+        ("bc7enc_least_squares", ctypes.c_uint8),
+        ("bc7enc_filterbank", ctypes.c_uint8),
     ]
 
 
@@ -77,6 +84,12 @@ class Options:
     bc7_quality: float = 1.0
     bc7_performance: float = 1.0
     bc7_shake_ranks: int = 0
+    # bc7enc16 (FMT_BC7ENC16): the image API's defaults (perceptual, fast = false -> uber level 4)
+    bc7enc_perceptual: bool = True
+    bc7enc_uber_level: int = 4
+    bc7enc_max_partitions: int = 64
+    bc7enc_least_squares: bool = True
+    bc7enc_filterbank: bool = True
 
     def to_c(self) -> _COptions:
         o = _COptions()
@@ -93,7 +106,18 @@ class Options:
         o.bc7_quality = float(self.bc7_quality)
         o.bc7_performance = float(self.bc7_performance)
         o.bc7_shake_ranks = int(self.bc7_shake_ranks)
+        o.bc7enc_perceptual = int(bool(self.bc7enc_perceptual))
+        o.bc7enc_uber_level = int(self.bc7enc_uber_level)
+        o.bc7enc_max_partitions = int(self.bc7enc_max_partitions)
+        o.bc7enc_least_squares = int(bool(self.bc7enc_least_squares))
+        o.bc7enc_filterbank = int(bool(self.bc7enc_filterbank))
         return o
+
+    @staticmethod
+    def bc7enc16(fast: bool = False, perceptual: bool = True) -> "Options":
+        """The settings Image_CompressRichGel999BC7enc16 derives from its
+        (fast, perceptual) arguments (richgel999_bc7enc16.cpp:73-89)."""
+        return Options(bc7enc_perceptual=perceptual, bc7enc_uber_level=0 if fast else 4)
 
 
 _lib = None
@@ -120,6 +144,8 @@ def library() -> ctypes.CDLL:
     lib.gic_hip_encode.restype = ctypes.c_int
     lib.gic_hip_encode_blocks_f32.argtypes = [ctypes.c_int, vp, u32, ctypes.POINTER(_COptions), vp, vp, vp]
     lib.gic_hip_encode_blocks_f32.restype = ctypes.c_int
+    lib.gic_hip_encode_blocks_u8.argtypes = [ctypes.c_int, vp, u32, ctypes.POINTER(_COptions), vp, vp]
+    lib.gic_hip_encode_blocks_u8.restype = ctypes.c_int
     lib.gic_hip_decode.argtypes = [ctypes.c_int, vp, u32, u32, u32, vp, sz, vp]
     lib.gic_hip_decode.restype = ctypes.c_int
     lib.gic_decompress_image.argtypes = [vp]
@@ -231,8 +257,8 @@ def encode_blocks_f32(fmt: int, blocks, dst, options: Options | None = None, blo
     ``Image_CompressAMDMultiModeLDRBlock`` (reference imagecompress.h:117-136).
     """
     import torch
-    if fmt not in (FMT_BC1, FMT_BC2, FMT_BC3, FMT_BC4, FMT_BC7):
-        raise GicError(f"encode_blocks_f32: format {fmt} has no block-level entry (BC1, BC2, BC3, BC4, BC7)")
+    if fmt not in (FMT_BC1, FMT_BC2, FMT_BC3, FMT_BC4, FMT_BC7, FMT_BC7ENC16):
+        raise GicError(f"encode_blocks_f32: format {fmt} has no block-level entry (BC1, BC2, BC3, BC4, BC7, BC7ENC16)")
     if not (blocks.is_cuda and dst.is_cuda):
         raise GicError("encode_blocks_f32 needs device (HBM) tensors; there is no CPU path")
     if blocks.dtype != torch.float32 or not blocks.is_contiguous():
@@ -253,6 +279,25 @@ def encode_blocks_f32(fmt: int, blocks, dst, options: Options | None = None, blo
                                              block_err.data_ptr() if block_err is not None else None,
                                              _stream_handle(stream))
     _check(rc)
+
+
+def encode_blocks_u8(blocks, dst, options: Options | None = None, stream=None) -> None:
+    """bc7enc16 at its block ABI (``Image_CompressRichGel999BC7enc16``, reference
+    imagecompress.h:139-142): blocks is a uint8 CUDA tensor (n, 64) of RGBA8
+    texels (or int32/uint32 (n, 16) packed words); dst receives n 16-byte BC7 blocks."""
+    import torch
+    if not (blocks.is_cuda and dst.is_cuda):
+        raise GicError("encode_blocks_u8 needs device (HBM) tensors; there is no CPU path")
+    if not blocks.is_contiguous() or blocks.dim() != 2 or blocks.numel() * blocks.element_size() != blocks.shape[0] * 64:
+        raise GicError("blocks must be a contiguous (n, 64) uint8 or (n, 16) 32-bit tensor")
+    n = blocks.shape[0]
+    if n == 0:
+        return
+    if not dst.is_contiguous() or dst.numel() * dst.element_size() < n * 16:
+        raise GicError(f"dst too small or not contiguous: need {n * 16} bytes")
+    opts = (options or Options()).to_c()
+    _check(library().gic_hip_encode_blocks_u8(FMT_BC7ENC16, blocks.data_ptr(), n, ctypes.byref(opts),
+                                              dst.data_ptr(), _stream_handle(stream)))
 
 
 def decode_device(fmt: int, blocks, width: int, height: int, slices: int, out, row_pitch: int | None = None,
@@ -333,3 +378,12 @@ def compress_bc7(image, options: Options | None = None):
     if image.ndim >= 3 and image.shape[-1] < 4:
         o = replace(o, force_alpha_one=True)
     return _host_compress(FMT_BC7, image, o)
+
+
+def compress_bc7_fast(image, options: Options | None = None):
+    """Image_CompressRichGel999BC7 (richgel999_bc7enc16.cpp:21-71): bc7enc16 with
+    the image API's defaults (perceptual, uber level 4) unless options say otherwise."""
+    o = options or Options()
+    if image.ndim >= 3 and image.shape[-1] < 4:
+        o = replace(o, force_alpha_one=True)
+    return _host_compress(FMT_BC7ENC16, image, o)

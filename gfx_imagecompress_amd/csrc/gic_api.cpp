@@ -42,6 +42,9 @@ hipError_t launch_bc4_blocks(const float *blocks, uint32_t n, void *dst, hipStre
 hipError_t launch_bc7_image(const Geometry &g, const gic_options &o, void *dst, double *err, hipStream_t s);
 hipError_t launch_bc7_blocks(const float *blocks, uint32_t n, const gic_options &o, void *dst, double *err,
                              hipStream_t s);
+hipError_t launch_bc7enc_image(const Geometry &g, const gic_options &o, void *dst, hipStream_t s);
+hipError_t launch_bc7enc_blocks_u8(const uint32_t *blocks, uint32_t n, const gic_options &o, void *dst, hipStream_t s);
+hipError_t launch_bc7enc_blocks_f32(const float *blocks, uint32_t n, const gic_options &o, void *dst, hipStream_t s);
 }  // namespace gic
 
 static thread_local int t_last_hip_error = 0;
@@ -70,6 +73,11 @@ extern "C" void gic_default_options(gic_options *o)
     o->alpha_restrict = 1;
     o->bc7_quality = 1.0f;
     o->bc7_performance = 1.0f;
+    o->bc7enc_perceptual = 1;                // richgel999_bc7enc16.cpp:13-19 ({perceptual, fast} = {true, false})
+    o->bc7enc_uber_level = 4;                // :79 (BC7ENC16_MAX_UBER_LEVEL unless fast)
+    o->bc7enc_max_partitions = 64;           // richgel999_bc7enc16.h:58
+    o->bc7enc_least_squares = 1;
+    o->bc7enc_filterbank = 1;
 }
 
 extern "C" uint32_t gic_block_bytes(gic_format fmt)
@@ -84,13 +92,14 @@ static int check_options(gic_format fmt, const gic_options &o)
     if (fmt == GIC_FMT_BC4 && o.bc4_channel > 3) return GIC_EINVAL;
     if (fmt == GIC_FMT_BC7 && o.bc7_performance != 1.0f) return GIC_EUNSUP;   // optQuantTrace_d path not built
     if (o.bc7_shake_ranks > 8) return GIC_EINVAL;
+    if (fmt == GIC_FMT_BC7ENC16 && (o.bc7enc_uber_level > 4 || o.bc7enc_max_partitions > 64)) return GIC_EINVAL;
     return GIC_OK;
 }
 
 static bool valid_fmt(gic_format f)
 {
     return f == GIC_FMT_BC1 || f == GIC_FMT_BC2 || f == GIC_FMT_BC3 || f == GIC_FMT_BC4 || f == GIC_FMT_BC5 ||
-           f == GIC_FMT_BC7;
+           f == GIC_FMT_BC7 || f == GIC_FMT_BC7ENC16;
 }
 
 extern "C" int gic_hip_encode_rows(gic_format fmt, const uint8_t *d_src, uint32_t width, uint32_t height,
@@ -127,7 +136,7 @@ extern "C" int gic_hip_encode_rows(gic_format fmt, const uint8_t *d_src, uint32_
     g.total = (uint32_t)total;
     hipStream_t s = (hipStream_t)stream;
     hipError_t e = hipSuccess;
-    if (d_block_err && fmt != GIC_FMT_BC7) {
+    if (d_block_err && fmt != GIC_FMT_BC7) {   // no encoder error but the AMD BC7 one
         e = hipMemsetAsync(d_block_err, 0, sizeof(double) * total, s);
         if (e != hipSuccess) return hip_fail(e);
     }
@@ -146,6 +155,9 @@ extern "C" int gic_hip_encode_rows(gic_format fmt, const uint8_t *d_src, uint32_
         break;
     case GIC_FMT_BC7:
         e = gic::launch_bc7_image(g, o, d_dst, d_block_err, s);
+        break;
+    case GIC_FMT_BC7ENC16:
+        e = gic::launch_bc7enc_image(g, o, d_dst, s);
         break;
     }
     if (e != hipSuccess) return hip_fail(e);
@@ -217,6 +229,9 @@ extern "C" int gic_hip_encode_rows_src(gic_format fmt, gic_source src_type, cons
         case GIC_FMT_BC7:
             e = gic::launch_bc7_blocks(tmp, n, o, out, d_block_err ? d_block_err + first : nullptr, s);
             break;
+        case GIC_FMT_BC7ENC16:
+            e = gic::launch_bc7enc_blocks_f32(tmp, n, o, out, s);
+            break;
         }
     }
     const hipError_t ef = hipFreeAsync(tmp, s);
@@ -238,7 +253,8 @@ extern "C" int gic_hip_encode_blocks_f32(gic_format fmt, const float *d_blocks, 
                                          uint8_t *d_dst, double *d_block_err, void *stream)
 {
     if (!d_blocks || !d_dst || !n) return GIC_EINVAL;
-    if (fmt != GIC_FMT_BC1 && fmt != GIC_FMT_BC2 && fmt != GIC_FMT_BC3 && fmt != GIC_FMT_BC4 && fmt != GIC_FMT_BC7)
+    if (fmt != GIC_FMT_BC1 && fmt != GIC_FMT_BC2 && fmt != GIC_FMT_BC3 && fmt != GIC_FMT_BC4 && fmt != GIC_FMT_BC7 &&
+        fmt != GIC_FMT_BC7ENC16)
         return GIC_EINVAL;
     gic_options o;
     gic_default_options(&o);
@@ -256,8 +272,28 @@ extern "C" int gic_hip_encode_blocks_f32(gic_format fmt, const float *d_blocks, 
         e = gic::launch_bc4_blocks(d_blocks, n, d_dst, s);
     else if (fmt == GIC_FMT_BC2 || fmt == GIC_FMT_BC3)
         e = gic::launch_bc23_blocks(d_blocks, n, (int)fmt, o.refinement_steps, o.b3d_refinement, d_dst, s);
-    else
+    else if (fmt == GIC_FMT_BC7ENC16) {
+        e = d_block_err ? hipMemsetAsync(d_block_err, 0, sizeof(double) * n, s) : hipSuccess;
+        if (e == hipSuccess) e = gic::launch_bc7enc_blocks_f32(d_blocks, n, o, d_dst, s);
+    } else
         e = gic::launch_bc7_blocks(d_blocks, n, o, d_dst, d_block_err, s);
+    if (e != hipSuccess) return hip_fail(e);
+    return GIC_OK;
+}
+
+extern "C" int gic_hip_encode_blocks_u8(gic_format fmt, const uint32_t *d_blocks, uint32_t n, const gic_options *opt,
+                                        uint8_t *d_dst, void *stream)
+{
+    if (fmt != GIC_FMT_BC7ENC16 || !d_blocks || !d_dst || !n) return GIC_EINVAL;
+    gic_options o;
+    gic_default_options(&o);
+    if (opt) {
+        if (opt->struct_size != sizeof(gic_options)) return GIC_EINVAL;
+        o = *opt;
+    }
+    int rc = check_options(fmt, o);
+    if (rc) return rc;
+    const hipError_t e = gic::launch_bc7enc_blocks_u8(d_blocks, n, o, d_dst, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e);
     return GIC_OK;
 }
@@ -267,7 +303,7 @@ extern "C" int gic_hip_decode(gic_format fmt, const uint8_t *d_blocks, uint32_t 
 {
     if (!valid_fmt(fmt) || !d_blocks || !d_rgba || !width || !height || !slices) return GIC_EINVAL;
     if (row_pitch < (size_t)width * 4) return GIC_EINVAL;
-    const hipError_t e = fmt == GIC_FMT_BC7
+    const hipError_t e = (fmt == GIC_FMT_BC7 || fmt == GIC_FMT_BC7ENC16)
                              ? gic::launch_bc7_decode(d_blocks, width, height, slices, d_rgba, row_pitch, (hipStream_t)stream)
                              : gic::launch_bcx_decode(d_blocks, (int)fmt, width, height, slices, d_rgba, row_pitch,
                                                       (hipStream_t)stream);
@@ -587,19 +623,40 @@ extern "C" Image_ImageHeader const *Image_CompressAMDBC3(Image_ImageHeader const
     return compress_bc23(src, GIC_FMT_BC3, amd, cb, user);
 }
 
-// Outside this release: BC6H and the bc7enc16 fast path
-// are exported for link compatibility and fail the way the reference reports
-// any failure (NULL).
+// Outside this release: BC6H is exported for link
+// compatibility and fails the way the reference reports any failure (NULL).
 extern "C" Image_ImageHeader const *Image_CompressAMDBC6H(Image_ImageHeader const *, Image_CompressAMDBackendOptions const *,
                                                           Image_CompressProgressFunc, void *)
 {
     return nullptr;
 }
-extern "C" Image_ImageHeader const *Image_CompressRichGel999BC7(Image_ImageHeader const *,
-                                                                Image_CompressRichGel999BackendOptions const *,
-                                                                Image_CompressProgressFunc, void *)
+
+// The bc7enc16 options of Image_CompressRichGel999BC7enc16 (richgel999_bc7enc16.cpp:73-89):
+// perceptual or linear weights; fast = uber level 0, otherwise 4.
+static void bc7enc_options(gic_options &o, bool fast, bool perceptual)
 {
-    return nullptr;
+    o.bc7enc_perceptual = perceptual;
+    o.bc7enc_uber_level = fast ? 0 : 4;
+    o.bc7enc_max_partitions = 64;
+    o.bc7enc_least_squares = 1;
+    o.bc7enc_filterbank = 1;
+}
+
+// richgel999_bc7enc16.cpp:21-71: NULL options mean {perceptual = true, fast = false}
+// (:13-19); sRGB sources give the sRGB destination; sources without alpha read alpha 1.
+extern "C" Image_ImageHeader const *Image_CompressRichGel999BC7(Image_ImageHeader const *src,
+                                                                Image_CompressRichGel999BackendOptions const *rich,
+                                                                Image_CompressProgressFunc cb, void *user)
+{
+    static Image_CompressRichGel999BackendOptions const kDefaultRich = {true, false};
+    if (!src) return nullptr;
+    rich = rich ? rich : &kDefaultRich;
+    TinyImageFormat f = TinyImageFormat_IsSRGB(src->format) ? TinyImageFormat_DXBC7_SRGB : TinyImageFormat_DXBC7_UNORM;
+    gic_options o;
+    gic_default_options(&o);
+    bc7enc_options(o, rich->fast, rich->perceptual);
+    o.force_alpha_one = TinyImageFormat_ChannelCount(src->format) > 3 ? 0 : 1;
+    return encode_host_image(src, GIC_FMT_BC7ENC16, f, o, cb, user);
 }
 
 // imagecompress.cpp:20-50 (the reference's trailing Deinit is unreachable)
@@ -721,7 +778,8 @@ extern "C" int gic_save_dds(Image_ImageHeader const *img, const char *path)
     case GIC_FMT_BC3: dxgi = srgb ? 78 : 77; break;
     case GIC_FMT_BC4: dxgi = snorm ? 81 : 80; break;
     case GIC_FMT_BC5: dxgi = snorm ? 84 : 83; break;
-    case GIC_FMT_BC7: dxgi = srgb ? 99 : 98; break;
+    case GIC_FMT_BC7:
+    case GIC_FMT_BC7ENC16: dxgi = srgb ? 99 : 98; break;
     }
     const uint32_t bb = gic_block_bytes(fmt);
     const uint32_t bx = (img->width + 3) / 4, by = (img->height + 3) / 4;
@@ -846,8 +904,21 @@ extern "C" void Image_CompressAMDExplictAlphaSingleModeBlock(float const alpha[1
     else
         memset(out, 0, 8);
 }
-extern "C" void Image_CompressRichGel999BC7enc16(uint32_t const *, bool, bool, void *out)
+// richgel999_bc7enc16.cpp:73-97: one block of 16 packed RGBA8 texels
+extern "C" void Image_CompressRichGel999BC7enc16(uint32_t const input[16], bool fast, bool perceptual, void *out)
 {
-    fprintf(stderr, "gfx_imagecompress_amd: Image_CompressRichGel999BC7enc16 is not implemented\n");
-    memset(out, 0, 16);
+    gic_options o;
+    gic_default_options(&o);
+    bc7enc_options(o, fast, perceptual);
+    DeviceScratch &s = t_scratch;
+    const bool ok = s.reserve(64, 16) &&
+                    hipMemcpyAsync(s.src, input, 64, hipMemcpyHostToDevice, s.stream) == hipSuccess &&
+                    gic_hip_encode_blocks_u8(GIC_FMT_BC7ENC16, (const uint32_t *)s.src, 1, &o, (uint8_t *)s.dst,
+                                             s.stream) == GIC_OK &&
+                    hipMemcpyAsync(out, s.dst, 16, hipMemcpyDeviceToHost, s.stream) == hipSuccess &&
+                    hipStreamSynchronize(s.stream) == hipSuccess;
+    if (!ok) {
+        fprintf(stderr, "gfx_imagecompress_amd: block encode failed on the GPU\n");
+        memset(out, 0, 16);
+    }
 }

@@ -1,0 +1,909 @@
+// gic_bc7enc.hip -- bc7enc16, the reference's fast BC7 encoder
+// (src/richgel999_bc7enc16.cpp, reached from ImageCompress_Compress(DXBC7,
+// fast = true), imagecompress.cpp:34-36), for CDNA4.
+//
+// Mapping: one lane per 4x4 block.  bc7enc16 is a short, branchy per-block
+// search (mode 6 over the whole block, then mode 1 on the one partition its
+// estimator picks), with no search breadth that would feed a whole wave per
+// block, so the 16 texels live in 16 VGPRs as packed RGBA8 words and every
+// step is lane-local.  Subsets are 16-bit texel masks walked in texel order,
+// so each float sum adds the same texels in the same order as the reference's
+// compacted lists (bit-exact under the numerics flags of gic_common.h).
+// Selectors are 4-bit nibbles of a 64-bit word.  The least-squares selector
+// weights and the single-colour table sit in LDS.
+//
+// Error arithmetic is 32-bit: the largest per-texel error (perceptual RGBA:
+// 512*510^2 + 103*803^2 + 18*946^2 + 128*255^2 < 2.3e8) times 16 texels stays
+// below 2^32, so the reference's uint64 totals never exceed 32 bits and
+// 0xffffffff can stand for its UINT64_MAX "no solution yet".
+#include "bc7_tables.h"
+#include "bc7enc_tables.h"
+#include "gic_common.h"
+
+namespace gic {
+namespace {
+
+constexpr uint32_t kNone = 0xffffffffu;
+
+struct EncCfg {                 // bc7enc16_compress_block_params (richgel999_bc7enc16.h:17-36)
+    uint32_t uber;              // m_uber_level 0..4
+    uint32_t max_parts;         // m_max_partitions_mode1 0..64
+    uint32_t lsq;               // m_try_least_squares
+    uint32_t filterbank;        // m_mode1_partition_estimation_filterbank
+    uint32_t w[4];              // error weights after bc7enc16_compress_block's scaling (:1524-1535)
+};
+
+struct EncLds {
+    float wx[96];               // g_bc7_weights3x (0..31), g_bc7_weights4x (32..95)
+    uint32_t one[512];          // g_bc7_mode_1_optimal_endpoints
+};
+
+__device__ __forceinline__ uint32_t ch(uint32_t c, int k) { return (c >> (8 * k)) & 0xffu; }
+__device__ __forceinline__ float clampf_r(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
+__device__ __forceinline__ float sat(float v) { return clampf_r(v, 0.f, 1.0f); }
+__device__ __forceinline__ int clampi_r(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+__device__ __forceinline__ uint32_t sel_at(uint64_t s, int i) { return (uint32_t)(s >> (4 * i)) & 15u; }
+
+// g_bc7_weights3/4 (:130-131): round(64 s / (N - 1))
+__device__ __forceinline__ uint32_t bc7w(uint32_t s, uint32_t N)
+{
+    return N == 16 ? (s * 64u + 7u) / 15u : (s * 64u + 3u) / 7u;
+}
+
+// interpolated channel k of the ramp point with weight w (:445, :1053)
+__device__ __forceinline__ int lerp_ch(uint32_t a, uint32_t b, int k, uint32_t w)
+{
+    return (int)((ch(a, k) * (64u - w) + ch(b, k) * w + 32u) >> 6);
+}
+
+struct Prob {           // one subset problem (color_cell_compressor_params :282-295)
+    uint32_t mask;      // texels of the subset
+    uint32_t n;         // its texel count
+    uint32_t nsel;      // 16 (mode 6) / 8 (mode 1)
+    uint32_t cbits;     // 7 / 6
+    bool mode1;         // shared p-bit, single-colour paths, degenerate-endpoint fix
+    bool alpha;         // RGBA (mode 6 of a block with alpha)
+};
+
+struct Res {            // color_cell_compressor_results :297-305
+    uint32_t err;
+    uint32_t lo, hi;    // quantised endpoints, channel k in byte k
+    uint32_t pb0, pb1;
+    uint64_t sel;       // selector of texel i in nibble i (texels of the subset only)
+};
+
+// per-texel transforms of the perceptual metric, computed once per block
+struct Ycc {
+    int l[16], cr[16], cb[16];
+};
+
+// scale_color :307-323 (n = component bits + p-bit)
+__device__ __forceinline__ uint32_t expand(uint32_t q, uint32_t n)
+{
+    uint32_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t v = ch(q, k) << (8 - n);
+        r |= ((v | (v >> n)) & 0xffu) << (8 * k);
+    }
+    return r;
+}
+
+// compute_color_distance_rgb / _rgba with perceptual = false (:325-355)
+__device__ __forceinline__ uint32_t lin_err(int r, int g, int b, int a, uint32_t c, bool alpha, const EncCfg &cf)
+{
+    const int dr = r - (int)ch(c, 0), dg = g - (int)ch(c, 1), db = b - (int)ch(c, 2);
+    uint32_t e = cf.w[0] * (uint32_t)(dr * dr) + cf.w[1] * (uint32_t)(dg * dg) + cf.w[2] * (uint32_t)(db * db);
+    if (alpha) {
+        const int da = a - (int)ch(c, 3);
+        e += cf.w[3] * (uint32_t)(da * da);
+    }
+    return e;
+}
+
+// the YCbCr-style transform of compute_color_distance_rgb (:331-339)
+__device__ __forceinline__ void ycc(int r, int g, int b, int &l, int &cr, int &cb)
+{
+    l = r * 109 + g * 366 + b * 37;
+    cr = (r << 9) - l;
+    cb = (b << 9) - l;
+}
+
+template <bool P>
+__device__ __forceinline__ uint32_t pair_err(int l1, int cr1, int cb1, int a1, int l2, int cr2, int cb2, int a2,
+                                             int r1, int g1, int b1, int r2, int g2, int b2, bool alpha,
+                                             const EncCfg &cf)
+{
+    int d0, d1, d2;
+    if (P) {
+        d0 = (l1 - l2) >> 8;
+        d1 = (cr1 - cr2) >> 8;
+        d2 = (cb1 - cb2) >> 8;
+    } else {
+        d0 = r1 - r2;
+        d1 = g1 - g2;
+        d2 = b1 - b2;
+    }
+    uint32_t e = cf.w[0] * (uint32_t)(d0 * d0) + cf.w[1] * (uint32_t)(d1 * d1) + cf.w[2] * (uint32_t)(d2 * d2);
+    if (alpha) e += cf.w[3] * (uint32_t)((a1 - a2) * (a1 - a2));
+    return e;
+}
+
+// evaluate_solution :405-572
+template <bool P>
+__device__ void evaluate(uint32_t lo, uint32_t hi, uint32_t pb0, uint32_t pb1, const Prob &pr, const uint32_t px[16], const Ycc &tx,
+                         const EncCfg &cf, Res &r)
+{
+    const uint32_t p1 = pr.mode1 ? pb0 : pb1;
+    uint32_t qlo = 0, qhi = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        qlo |= ((ch(lo, k) << 1) | pb0) << (8 * k);
+        qhi |= ((ch(hi, k) << 1) | p1) << (8 * k);
+    }
+    const uint32_t a = expand(qlo, pr.cbits + 1), b = expand(qhi, pr.cbits + 1);
+    const uint32_t N = pr.nsel;
+    uint32_t tot = 0;
+    uint64_t ts = 0;
+    if (!P) {
+        const int ar = ch(a, 0), ag = ch(a, 1), ab = ch(a, 2), aa = ch(a, 3);
+        const int dr = (int)ch(b, 0) - ar, dg = (int)ch(b, 1) - ag, db = (int)ch(b, 2) - ab;
+        const int da = pr.alpha ? (int)ch(b, 3) - aa : 0;
+        const float f = N / (float)(dr * dr + dg * dg + db * db + da * da + .00000125f);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            if (!((pr.mask >> i) & 1u)) continue;
+            const uint32_t c = px[i];
+            int dot = ((int)ch(c, 0) - ar) * dr + ((int)ch(c, 1) - ag) * dg + ((int)ch(c, 2) - ab) * db;
+            if (pr.alpha) dot += ((int)ch(c, 3) - aa) * da;
+            int s = (int)((float)dot * f + .5f);
+            s = clampi_r(s, 1, (int)N - 1);
+            const uint32_t w0 = bc7w(s - 1, N), w1 = bc7w(s, N);
+            const uint32_t e0 = lin_err(lerp_ch(a, b, 0, w0), lerp_ch(a, b, 1, w0), lerp_ch(a, b, 2, w0),
+                                        lerp_ch(a, b, 3, w0), c, pr.alpha, cf);
+            const uint32_t e1 = lin_err(lerp_ch(a, b, 0, w1), lerp_ch(a, b, 1, w1), lerp_ch(a, b, 2, w1),
+                                        lerp_ch(a, b, 3, w1), c, pr.alpha, cf);
+            // both reference branches move down exactly when err0 < err1 (:479, :508)
+            if (e0 < e1) {
+                tot += e0;
+                --s;
+            } else {
+                tot += e1;
+            }
+            ts |= (uint64_t)s << (4 * i);
+        }
+    } else {
+        // ramp point outer (a real loop), texels inner: each texel keeps its first
+        // minimum as the reference's per-texel scan does (:522-555)
+        uint32_t be[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) be[i] = kNone;
+#pragma unroll 1
+        for (uint32_t j = 0; j < N; ++j) {
+            const uint32_t w = bc7w(j, N);
+            int l1, cr1, cb1;
+            ycc(lerp_ch(a, b, 0, w), lerp_ch(a, b, 1, w), lerp_ch(a, b, 2, w), l1, cr1, cb1);
+            const int a1 = lerp_ch(a, b, 3, w);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                if (!((pr.mask >> i) & 1u)) continue;
+                const uint32_t e = pair_err<true>(l1, cr1, cb1, a1, tx.l[i], tx.cr[i], tx.cb[i], (int)ch(px[i], 3), 0,
+                                                  0, 0, 0, 0, 0, pr.alpha, cf);
+                if (e < be[i]) {
+                    be[i] = e;
+                    ts = (ts & ~((uint64_t)15u << (4 * i))) | ((uint64_t)j << (4 * i));
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if ((pr.mask >> i) & 1u) tot += be[i];
+    }
+    if (tot < r.err) {
+        r.err = tot;
+        r.lo = lo;
+        r.hi = hi;
+        r.pb0 = pb0;
+        r.pb1 = pb1;
+        r.sel = ts;
+    }
+}
+
+// find_optimal_solution :606-729 (modes 1 and 6 both carry p-bits) with
+// fixDegenerateEndpoints :574-604 (mode 1)
+template <bool P>
+__device__ void fit(float xl[4], float xh[4], const Prob &pr, const uint32_t px[16], const Ycc &tx, const EncCfg &cf, Res &r)
+{
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xl[k] = sat(xl[k]), xh[k] = sat(xh[k]);
+    const int iscalep = (1 << (pr.cbits + 1)) - 1;
+    const float scalep = (float)iscalep;
+    const uint32_t nb = pr.cbits + 1;
+    uint32_t bmin = 0, bmax = 0, bp0 = 0, bp1 = 0;
+    if (!pr.mode1) {
+        float be0 = 1e+9f, be1 = 1e+9f;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            uint32_t qa = 0, qb = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                qa |= (uint32_t)clampi_r(((int)((xl[k] * scalep - p) / 2.0f + .5f)) * 2 + p, p, iscalep - 1 + p)
+                      << (8 * k);
+                qb |= (uint32_t)clampi_r(((int)((xh[k] * scalep - p) / 2.0f + .5f)) * 2 + p, p, iscalep - 1 + p)
+                      << (8 * k);
+            }
+            const uint32_t sa = expand(qa, nb), sb = expand(qb, nb);
+            float e0 = 0, e1 = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (k == 3 && !pr.alpha) break;
+                const float t0 = (int)ch(sa, k) - xl[k] * 255.0f, t1 = (int)ch(sb, k) - xh[k] * 255.0f;
+                e0 += t0 * t0;
+                e1 += t1 * t1;
+            }
+            if (e0 < be0) be0 = e0, bp0 = (uint32_t)p, bmin = (qa >> 1) & 0x7f7f7f7fu;
+            if (e1 < be1) be1 = e1, bp1 = (uint32_t)p, bmax = (qb >> 1) & 0x7f7f7f7fu;
+        }
+    } else {
+        float be = 1e+9f;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            uint32_t qa = 0, qb = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                qa |= (uint32_t)clampi_r(((int)((xl[k] * scalep - p) / 2.0f + .5f)) * 2 + p, p, iscalep - 1 + p)
+                      << (8 * k);
+                qb |= (uint32_t)clampi_r(((int)((xh[k] * scalep - p) / 2.0f + .5f)) * 2 + p, p, iscalep - 1 + p)
+                      << (8 * k);
+            }
+            const uint32_t sa = expand(qa, nb), sb = expand(qb, nb);
+            float e = 0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const float t0 = ((int)ch(sa, k) / 255.0f) - xl[k], t1 = ((int)ch(sb, k) / 255.0f) - xh[k];
+                e += t0 * t0 + t1 * t1;
+            }
+            if (e < be) be = e, bp0 = bp1 = (uint32_t)p, bmin = (qa >> 1) & 0x7f7f7f7fu, bmax = (qb >> 1) & 0x7f7f7f7fu;
+        }
+        const uint32_t isc = (uint32_t)(iscalep >> 1);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            uint32_t mn = ch(bmin, k), mx = ch(bmax, k);
+            if (mn != mx || !(fabsf(xl[k] - xh[k]) > 0.0f)) continue;
+            if (mn > (isc >> 1)) {
+                if (mn > 0)
+                    mn--;
+                else if (mx < isc)
+                    mx++;
+            } else {
+                if (mx < isc)
+                    mx++;
+                else if (mn > 0)
+                    mn--;
+            }
+            bmin = (bmin & ~(0xffu << (8 * k))) | (mn << (8 * k));
+            bmax = (bmax & ~(0xffu << (8 * k))) | (mx << (8 * k));
+        }
+    }
+    if (r.err == kNone || bmin != r.lo || bmax != r.hi || bp0 != r.pb0 || bp1 != r.pb1)
+        evaluate<P>(bmin, bmax, bp0, bp1, pr, px, tx, cf, r);
+}
+
+// compute_least_squares_endpoints_rgb / _rgba :197-280, then the 1/255 scale
+__device__ void lsq(const Prob &pr, uint64_t sel, const uint32_t px[16], const EncLds &L, float xl[4], float xh[4])
+{
+    const float *wx = L.wx + (pr.nsel == 16 ? 32 : 0);
+    float z00 = 0.0f, z10 = 0.0f, z11 = 0.0f;
+    float q00[4] = {0.f, 0.f, 0.f, 0.f}, t[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (!((pr.mask >> i) & 1u)) continue;
+        const float *w4 = wx + 4 * sel_at(sel, i);
+        z00 += w4[0];
+        z10 += w4[1];
+        z11 += w4[2];
+        const float w = w4[3];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float c = (float)ch(px[i], k);
+            q00[k] += w * c;
+            t[k] += c;
+        }
+    }
+    const float z01 = z10;
+    float det = z00 * z11 - z01 * z10;
+    if (det != 0.0f) det = 1.0f / det;
+    const float i00 = z11 * det, i01 = -z01 * det, i10 = -z10 * det, i11 = z00 * det;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float q10 = t[k] - q00[k];
+        float l = i00 * q00[k] + i01 * q10, h = i10 * q00[k] + i11 * q10;
+        if (k == 3 && !pr.alpha) l = h = 255.0f;
+        xl[k] = l * (1.0f / 255.0f);
+        xh[k] = h * (1.0f / 255.0f);
+    }
+}
+
+// pack_mode1_to_one_color :357-403
+template <bool P>
+__device__ void one_colour(uint32_t cr, uint32_t cg, uint32_t cb, const Prob &pr, const uint32_t px[16], const Ycc &tx,
+                           const EncCfg &cf, const EncLds &L, Res &r)
+{
+    uint32_t best = kNone, bp = 0;
+#pragma unroll
+    for (uint32_t p = 0; p < 2; ++p) {
+        const uint32_t e = (L.one[cr * 2 + p] & 0xffffu) + (L.one[cg * 2 + p] & 0xffffu) + (L.one[cb * 2 + p] & 0xffffu);
+        if (e < best) best = e, bp = p;
+    }
+    const uint32_t er = L.one[cr * 2 + bp], eg = L.one[cg * 2 + bp], eb = L.one[cb * 2 + bp];
+    r.lo = ((er >> 16) & 0xffu) | (((eg >> 16) & 0xffu) << 8) | (((eb >> 16) & 0xffu) << 16);
+    r.hi = (er >> 24) | ((eg >> 24) << 8) | ((eb >> 24) << 16);
+    r.pb0 = bp;
+    r.pb1 = 0;
+    int q[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        uint32_t lo = ((ch(r.lo, k) << 1) | bp) << 1;
+        lo |= lo >> 7;
+        uint32_t hi = ((ch(r.hi, k) << 1) | bp) << 1;
+        hi |= hi >> 7;
+        q[k] = (int)((lo * (64u - 18u) + hi * 18u + 32u) >> 6);
+    }
+    int ql, qcr, qcb;
+    ycc(q[0], q[1], q[2], ql, qcr, qcb);
+    uint32_t tot = 0;
+    uint64_t ts = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (!((pr.mask >> i) & 1u)) continue;
+        const uint32_t c = px[i];
+        tot += pair_err<P>(ql, qcr, qcb, 0, tx.l[i], tx.cr[i], tx.cb[i], 0, q[0], q[1], q[2], ch(c, 0), ch(c, 1), ch(c, 2), false, cf);
+        ts |= (uint64_t)2u << (4 * i);
+    }
+    r.sel = ts;
+    r.err = tot;
+}
+
+// color_cell_compression :731-1024
+template <bool P>
+__device__ Res cell(const Prob &pr, const uint32_t px[16], const Ycc &tx, const EncCfg &cf, const EncLds &L)
+{
+    Res r;
+    r.err = kNone;
+    r.lo = r.hi = r.pb0 = r.pb1 = 0;
+    r.sel = 0;
+    if (pr.mode1) {   // the subset is one colour: pack it directly (:738-754)
+        uint32_t first = 0;
+        bool seen = false, same = true;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            if (!((pr.mask >> i) & 1u)) continue;
+            if (!seen) first = px[i] & 0xffffffu, seen = true;
+            same = same && (px[i] & 0xffffffu) == first;
+        }
+        if (same) {
+            one_colour<P>(ch(first, 0), ch(first, 1), ch(first, 2), pr, px, tx, cf, L, r);
+            return r;
+        }
+    }
+    // mean and principal axis (:756-841)
+    float m[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (!((pr.mask >> i) & 1u)) continue;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m[k] = m[k] + (float)ch(px[i], k);
+    }
+    float ms[4], mn[4], ax[4] = {0.f, 0.f, 0.f, 0.f};
+    const float inv_n = 1.0f / (float)pr.n, inv_n255 = 1.0f / (float)(pr.n * 255.0f);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ms[k] = m[k] * inv_n, mn[k] = sat(m[k] * inv_n255);
+    if (pr.alpha) {   // incremental PCA (:773-790)
+        bool seen = false;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            if (!((pr.mask >> i) & 1u)) continue;
+            float c[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) c[k] = (float)ch(px[i], k) - ms[k];
+            float n[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) n[k] = seen ? ax[k] : c[k];
+            seen = true;
+            float s = n[0] * n[0] + n[1] * n[1] + n[2] * n[2] + n[3] * n[3];
+            if (s != 0.0f) {
+                s = 1.0f / sqrtf(s);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) n[k] *= s;
+            }
+            float add[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float a0 = c[0] * c[q], a1 = c[1] * c[q], a2 = c[2] * c[q], a3 = c[3] * c[q];
+                add[q] = a0 * n[0] + a1 * n[1] + a2 * n[2] + a3 * n[3];
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ax[q] += add[q];
+        }
+        float s = ax[0] * ax[0] + ax[1] * ax[1] + ax[2] * ax[2] + ax[3] * ax[3];
+        if (s != 0.0f) {
+            s = 1.0f / sqrtf(s);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ax[k] *= s;
+        }
+    } else {   // covariance and three power steps (:795-831)
+        float cv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            if (!((pr.mask >> i) & 1u)) continue;
+            const float r0 = (int)ch(px[i], 0) - ms[0], g0 = (int)ch(px[i], 1) - ms[1], b0 = (int)ch(px[i], 2) - ms[2];
+            cv[0] += r0 * r0, cv[1] += r0 * g0, cv[2] += r0 * b0, cv[3] += g0 * g0, cv[4] += g0 * b0, cv[5] += b0 * b0;
+        }
+        float vr = .9f, vg = 1.0f, vb = .7f;
+#pragma unroll
+        for (int it = 0; it < 3; ++it) {
+            float x = vr * cv[0] + vg * cv[1] + vb * cv[2];
+            float y = vr * cv[1] + vg * cv[3] + vb * cv[4];
+            float z = vr * cv[2] + vg * cv[4] + vb * cv[5];
+            const float ax0 = fabsf(x), ay0 = fabsf(y), az0 = fabsf(z);
+            const float mxy = ax0 > ay0 ? ax0 : ay0;
+            float mm = mxy > az0 ? mxy : az0;
+            if (mm > 1e-10f) {
+                mm = 1.0f / mm;
+                x *= mm, y *= mm, z *= mm;
+            }
+            vr = x, vg = y, vb = z;
+        }
+        float len = vr * vr + vg * vg + vb * vb;
+        if (!(len < 1e-10f)) {
+            len = 1.0f / sqrtf(len);
+            ax[0] = vr * len, ax[1] = vg * len, ax[2] = vb * len;
+        }
+    }
+    if (ax[0] * ax[0] + ax[1] * ax[1] + ax[2] * ax[2] + ax[3] * ax[3] < .5f) {
+        if (P)
+            ax[0] = .213f, ax[1] = .715f, ax[2] = .072f, ax[3] = pr.alpha ? .715f : 0.f;
+        else
+            ax[0] = 1.0f, ax[1] = 1.0f, ax[2] = 1.0f, ax[3] = pr.alpha ? 1.0f : 0.f;
+        float s = ax[0] * ax[0] + ax[1] * ax[1] + ax[2] * ax[2] + ax[3] * ax[3];
+        if (s != 0.0f) {
+            s = 1.0f / sqrtf(s);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ax[k] *= s;
+        }
+    }
+    float lo = 1e+9f, hi = -1e+9f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (!((pr.mask >> i) & 1u)) continue;
+        float q[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[k] = (float)ch(px[i], k) - ms[k];
+        const float d = q[0] * ax[0] + q[1] * ax[1] + q[2] * ax[2] + q[3] * ax[3];
+        lo = lo < d ? lo : d;
+        hi = hi > d ? hi : d;
+    }
+    lo *= (1.0f / 255.0f);
+    hi *= (1.0f / 255.0f);
+    float cmin[4], cmax[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cmin[k] = sat(mn[k] + ax[k] * lo), cmax[k] = sat(mn[k] + ax[k] * hi);
+    if (cmin[0] * 1.0f + cmin[1] * 1.0f + cmin[2] * 1.0f + cmin[3] * 1.0f >
+        cmax[0] * 1.0f + cmax[1] * 1.0f + cmax[2] * 1.0f + cmax[3] * 1.0f) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float t = cmin[k];
+            cmin[k] = cmax[k];
+            cmax[k] = t;
+        }
+    }
+
+    // Trials, each a fit that keeps the best (:874-1006): t = 0 the PCA endpoints;
+    // then the least-squares refit of the current selectors; uber >= 1: refits of
+    // the snapshot with its minimum selectors raised, its maximum lowered, both;
+    // uber >= 2 and error above (n*56)>>4: refits of rescaled snapshots over
+    // ly in [-Q, 1] x hy in [max-1, max+Q] without (0, max).
+    const int nls = cf.lsq ? 1 : 0;
+    const int nub = cf.uber > 0 ? 3 : 0;
+    const int Q = cf.uber >= 4 ? (int)cf.uber - 2 : 1;
+    const int ngrid = cf.uber >= 2 ? (Q + 2) * (Q + 2) - 1 : 0;
+    const int ntr = 1 + nls + nub + ngrid;
+    const int maxs = (int)pr.nsel - 1;
+    bool zero = false, grid = false;
+    uint64_t base = 0;
+    uint32_t smin = 16, smax = 0;
+    for (int t = 0; t < ntr; ++t) {
+        if (zero) break;   // color_cell_compression returns 0 at once
+        if (t == 1 + nls) {
+            base = r.sel;
+            smin = 16, smax = 0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                if (!((pr.mask >> i) & 1u)) continue;
+                const uint32_t s = sel_at(base, i);
+                smin = s < smin ? s : smin;
+                smax = s > smax ? s : smax;
+            }
+        }
+        if (t == 1 + nls + nub) grid = r.err > ((pr.n * 56u) >> 4);
+        if (t >= 1 + nls + nub && !grid) break;
+        float xl[4], xh[4];
+        if (t == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) xl[k] = cmin[k], xh[k] = cmax[k];
+        } else {
+            uint64_t ts = 0;
+            if (t <= nls) {
+                ts = r.sel;
+            } else if (t < 1 + nls + nub) {
+                const int u = t - 1 - nls;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    if (!((pr.mask >> i) & 1u)) continue;
+                    uint32_t s = sel_at(base, i);
+                    if (u != 1 && s == smin && s < pr.nsel - 1)
+                        s++;
+                    else if (u != 0 && s == smax && s > 0)
+                        s--;
+                    ts |= (uint64_t)s << (4 * i);
+                }
+            } else {
+                int g = t - (1 + nls + nub);
+                if (g >= Q * (Q + 2) + 1) ++g;   // skip (ly, hy) = (0, max)
+                const int ly = -Q + g / (Q + 2), hy = maxs - 1 + g % (Q + 2);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    if (!((pr.mask >> i) & 1u)) continue;
+                    const float v = floorf((float)maxs * ((float)sel_at(base, i) - (float)ly) / ((float)hy - (float)ly) +
+                                           .5f);
+                    ts |= (uint64_t)(uint32_t)clampf_r(v, 0, (float)maxs) << (4 * i);
+                }
+            }
+            lsq(pr, ts, px, L, xl, xh);
+        }
+        fit<P>(xl, xh, pr, px, tx, cf, r);
+        zero = r.err == 0;
+    }
+    if (!zero && pr.mode1) {   // the subset mean as one colour (:1009-1021)
+        Res avg = r;
+        one_colour<P>((uint32_t)(int)(.5f + mn[0] * 255.0f), (uint32_t)(int)(.5f + mn[1] * 255.0f),
+                      (uint32_t)(int)(.5f + mn[2] * 255.0f), pr, px, tx, cf, L, avg);
+        if (avg.err < r.err) r = avg;
+    }
+    return r;
+}
+
+// color_cell_compression_est :1026-1162 for the texels of `mask` (full sums:
+// the reference's partial-sum exits only ever make a candidate lose a '<' test)
+template <bool P>
+__device__ uint32_t estimate(uint32_t mask, const uint32_t px[16], const Ycc &tx, const EncCfg &cf)
+{
+    int lo[3] = {255, 255, 255}, hi[3] = {0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (!((mask >> i) & 1u)) continue;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int v = ch(px[i], k);
+            lo[k] = v < lo[k] ? v : lo[k];
+            hi[k] = v > hi[k] ? v : hi[k];
+        }
+    }
+    const int ar = hi[0] - lo[0], ag = hi[1] - lo[1], ab = hi[2] - lo[2];
+    int th[7], prev = lo[0] * ar + lo[1] * ag + lo[2] * ab;
+#pragma unroll
+    for (int s = 1; s < 8; ++s) {
+        const int w = (int)bc7w((uint32_t)s, 8);
+        const int r = (lo[0] * (64 - w) + hi[0] * w + 32) >> 6, g = (lo[1] * (64 - w) + hi[1] * w + 32) >> 6,
+                  b = (lo[2] * (64 - w) + hi[2] * w + 32) >> 6;
+        const int d = r * ar + g * ag + b * ab;
+        th[s - 1] = (prev + d + 1) >> 1;
+        prev = d;
+    }
+    uint32_t tot = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (!((mask >> i) & 1u)) continue;
+        const int cr = ch(px[i], 0), cg = ch(px[i], 1), cb = ch(px[i], 2);
+        const int d = ar * cr + ag * cg + ab * cb;
+        int s = 0;   // the dots of the ramp rise with s, so the first threshold from the top is a count
+#pragma unroll
+        for (int k = 0; k < 7; ++k) s += d >= th[k];
+        const int w = (int)bc7w((uint32_t)s, 8);
+        const int r = (lo[0] * (64 - w) + hi[0] * w + 32) >> 6, g = (lo[1] * (64 - w) + hi[1] * w + 32) >> 6,
+                  b = (lo[2] * (64 - w) + hi[2] * w + 32) >> 6;
+        if (P) {
+            int l1, cr1, cb1;
+            ycc(r, g, b, l1, cr1, cb1);
+            tot += (uint32_t)(int)pair_err<true>(l1, cr1, cb1, 0, tx.l[i], tx.cr[i], tx.cb[i], 0, 0, 0, 0, 0, 0, 0,
+                                                 false, cf);
+        } else {
+            tot += pair_err<false>(0, 0, 0, 0, 0, 0, 0, 0, r, g, b, cr, cg, cb, false, cf);
+        }
+    }
+    return tot;
+}
+
+__device__ __forceinline__ uint32_t shape_mask(uint32_t shape, uint32_t subset)
+{
+    uint32_t m = 0;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) m |= (((shape >> (2 * t)) & 3u) == subset ? 1u : 0u) << t;
+    return m;
+}
+
+// estimate_partition :1207-1281
+template <bool P>
+__device__ uint32_t pick_partition(const uint32_t px[16], const Ycc &tx, const EncCfg &cf)
+{
+    const uint32_t total = cf.max_parts < 64 ? cf.max_parts : 64;
+    if (total <= 1) return 0;
+    uint32_t best = kNone, best_part = 0, key = 0;
+    bool stop = false;
+    for (uint32_t it = 0; it < total; ++it) {
+        if (stop || best == 0) break;
+        const uint32_t part = kEncPartOrder[it];
+        if (cf.filterbank && it >= 14 && it <= 34 && !(kEncPredictors[part] & (1u << (key + 1)))) {
+            if (it == 34) stop = true;
+            continue;
+        }
+        const uint32_t m0 = shape_mask(kBc7Shape2[part], 0);
+        const uint32_t e = estimate<P>(m0, px, tx, cf) + estimate<P>(~m0 & 0xffffu, px, tx, cf);
+        if (e < best) best = e, best_part = part;
+        if (part == 34 && best_part != 34) stop = true;
+        if (it == 13) key = best_part;
+    }
+    return best_part;
+}
+
+// 128-bit little-endian bit writer (set_block_bits :1283-1295)
+struct Bits {
+    uint64_t w0 = 0, w1 = 0;
+    uint32_t pos = 0;
+    __device__ void put(uint32_t v, uint32_t n)
+    {
+        const uint64_t x = (uint64_t)v;
+        if (pos < 64) {
+            w0 |= x << pos;
+            if (pos + n > 64) w1 |= x >> (64 - pos);
+        } else {
+            w1 |= x << (pos - 64);
+        }
+        pos += n;
+    }
+};
+
+// encode_bc7_block :1307-1388 for mode 6 (one subset) or mode 1 (partition `part`)
+__device__ uint4 pack_block(bool mode1, uint32_t part, uint64_t sel, const uint32_t lo[2], const uint32_t hi[2],
+                            uint32_t pb[2][2])
+{
+    const uint32_t shape = mode1 ? kBc7Shape2[part] : 0u;
+    const uint32_t ib = mode1 ? 3 : 4, nsub = mode1 ? 2 : 1;
+    const uint32_t anc1 = mode1 ? kBc7Anchor2[part] : 0xffu;
+    uint32_t l[2] = {lo[0], lo[1]}, h[2] = {hi[0], hi[1]};
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) {
+        if (k >= nsub) break;
+        const uint32_t a = k ? anc1 : 0;
+        if (!((uint32_t)(sel >> (4 * a)) & (1u << (ib - 1)))) continue;
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+            if (((shape >> (2 * t)) & 3u) == k) sel ^= (uint64_t)((1u << ib) - 1) << (4 * t);
+        const uint32_t tl = l[k];
+        l[k] = h[k];
+        h[k] = tl;
+        if (!mode1) {
+            const uint32_t tp = pb[k][0];
+            pb[k][0] = pb[k][1];
+            pb[k][1] = tp;
+        }
+    }
+    Bits b;
+    if (mode1) {
+        b.put(2u, 2);
+        b.put(part, 6);
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+            for (int k = 0; k < 2; ++k) b.put(ch(l[k], c), 6), b.put(ch(h[k], c), 6);
+        b.put(pb[0][0], 1);
+        b.put(pb[1][0], 1);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) b.put(sel_at(sel, t), (t == 0 || (uint32_t)t == anc1) ? 2 : 3);
+    } else {
+        b.put(64u, 7);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) b.put(ch(l[0], c), 7), b.put(ch(h[0], c), 7);
+        b.put(pb[0][0], 1);
+        b.put(pb[0][1], 1);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) b.put(sel_at(sel, t), t == 0 ? 3 : 4);
+    }
+    return make_uint4((uint32_t)b.w0, (uint32_t)(b.w0 >> 32), (uint32_t)b.w1, (uint32_t)(b.w1 >> 32));
+}
+
+// bc7enc16_compress_block :1517-1547 with handle_alpha_block / handle_opaque_block
+// :1390-1515 (m_endpoints_share_pbit, uninitialised for alpha blocks in the
+// reference, is false: mode 6 has a p-bit per endpoint)
+template <bool P>
+__device__ uint4 encode_block(const uint32_t px[16], const EncCfg &cf, const EncLds &L)
+{
+    Ycc tx;
+    if (P) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) ycc(ch(px[i], 0), ch(px[i], 1), ch(px[i], 2), tx.l[i], tx.cr[i], tx.cb[i]);
+    }
+    bool alpha = false;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) alpha = alpha || (px[i] >> 24) < 255u;
+    Res r6, s0, s1;
+    s0.err = s1.err = kNone;
+    bool mode1 = false;
+    uint32_t part = 0, m0 = 0xffffu;
+    // problem 0: mode 6 on the block; 1, 2: the two subsets of mode 1's partition
+    for (int prob = 0; prob < 3; ++prob) {
+        Prob pr;
+        if (prob == 0) {
+            pr.mask = 0xffffu, pr.n = 16, pr.nsel = 16, pr.cbits = 7, pr.mode1 = false, pr.alpha = alpha;
+        } else {
+            if (alpha || r6.err == 0 || cf.max_parts == 0) break;
+            if (prob == 1) {
+                part = pick_partition<P>(px, tx, cf);
+                m0 = shape_mask(kBc7Shape2[part], 0);
+            } else if (s0.err > r6.err) {
+                break;   // the reference stops once the first subset alone loses
+            }
+            pr.mask = prob == 1 ? m0 : (~m0 & 0xffffu);
+            pr.n = (uint32_t)__popc(pr.mask), pr.nsel = 8, pr.cbits = 6, pr.mode1 = true, pr.alpha = false;
+        }
+        const Res r = cell<P>(pr, px, tx, cf, L);
+        if (prob == 0)
+            r6 = r;
+        else if (prob == 1)
+            s0 = r;
+        else if (s0.err + r.err < r6.err)
+            mode1 = true, s1 = r;
+    }
+    uint32_t lo[2], hi[2], pb[2][2];
+    uint64_t sel;
+    if (mode1) {
+        sel = s0.sel | s1.sel;   // each subset's selectors sit in its own texels' nibbles
+        lo[0] = s0.lo, hi[0] = s0.hi, pb[0][0] = s0.pb0, pb[0][1] = 0;
+        lo[1] = s1.lo, hi[1] = s1.hi, pb[1][0] = s1.pb0, pb[1][1] = 0;
+    } else {
+        sel = r6.sel;
+        lo[0] = r6.lo, hi[0] = r6.hi, pb[0][0] = r6.pb0, pb[0][1] = r6.pb1;
+        lo[1] = hi[1] = pb[1][0] = pb[1][1] = 0;
+    }
+    return pack_block(mode1, part, sel, lo, hi, pb);
+}
+
+// ---- kernels ---------------------------------------------------------------
+
+__device__ __forceinline__ void load_tables(EncLds &L)
+{
+    for (uint32_t i = threadIdx.x; i < 96; i += blockDim.x)
+        L.wx[i] = __uint_as_float(i < 32 ? kEncW3x[i] : kEncW4x[i - 32]);
+    for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) L.one[i] = kEncOneColour[i];
+    __syncthreads();
+}
+
+// Image_CompressRichGel999BC7 :21-71 over 8-bit texels (its float round trip
+// v/255.0f -> R8G8B8A8_UNORM gives back the bytes)
+template <bool P>
+__global__ void __launch_bounds__(256) bc7enc_image_kernel(Geometry g, EncCfg cf, int force_alpha_one,
+                                                           uint4 *__restrict__ dst)
+{
+    __shared__ EncLds L;
+    load_tables(L);
+    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= g.total) return;
+    uint32_t slice, by, bx;
+    block_coords(g, id, slice, by, bx);
+    uint32_t px[16];
+    load_block_u8(g, slice, by, bx, force_alpha_one != 0, px);
+    dst[id] = encode_block<P>(px, cf, L);
+}
+
+// Image_CompressRichGel999BC7enc16 :73-97: blocks of 16 packed RGBA8 words
+template <bool P>
+__global__ void __launch_bounds__(256) bc7enc_blocks_kernel(const uint4 *__restrict__ blocks, uint32_t n, EncCfg cf,
+                                                            uint4 *__restrict__ dst)
+{
+    __shared__ EncLds L;
+    load_tables(L);
+    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= n) return;
+    uint32_t px[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint4 v = blocks[(size_t)id * 4 + q];
+        px[q * 4 + 0] = v.x, px[q * 4 + 1] = v.y, px[q * 4 + 2] = v.z, px[q * 4 + 3] = v.w;
+    }
+    dst[id] = encode_block<P>(px, cf, L);
+}
+
+// float RGBA blocks (the gic_hip_encode_rows_src / block-ABI path): each texel
+// to RGBA8 as saturate(v) * 255 + 0.5 truncated (TinyImageFormat's UNORM8 encode
+// is un-vendored; this rounding is unpinned and is the identity on v / 255.0f)
+template <bool P>
+__global__ void __launch_bounds__(256) bc7enc_f32_kernel(const float *__restrict__ blocks, uint32_t n, EncCfg cf,
+                                                         uint4 *__restrict__ dst)
+{
+    __shared__ EncLds L;
+    load_tables(L);
+    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= n) return;
+    uint32_t px[16];
+    const float4 *b = reinterpret_cast<const float4 *>(blocks) + (size_t)id * 16;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        const float4 v = b[t];
+        const float c[4] = {v.x, v.y, v.z, v.w};
+        uint32_t w = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w |= (uint32_t)(sat(c[k]) * 255.0f + 0.5f) << (8 * k);
+        px[t] = w;
+    }
+    dst[id] = encode_block<P>(px, cf, L);
+}
+
+EncCfg make_cfg(const gic_options &o)
+{
+    EncCfg c;
+    c.uber = o.bc7enc_uber_level;
+    c.max_parts = o.bc7enc_max_partitions;
+    c.lsq = o.bc7enc_least_squares;
+    c.filterbank = o.bc7enc_filterbank;
+    if (o.bc7enc_perceptual) {   // bc7enc16_compress_block_params_init_perceptual_weights + :1524-1532
+        const volatile float pr = (.5f / (1.0f - .2126f)) * (.5f / (1.0f - .2126f));
+        const volatile float pb = (.5f / (1.0f - .0722f)) * (.5f / (1.0f - .0722f));
+        c.w[0] = (uint32_t)(int)(128u * 4.0f);
+        c.w[1] = (uint32_t)(int)(64u * 4.0f * pr);
+        c.w[2] = (uint32_t)(int)(16u * 4.0f * pb);
+        c.w[3] = 32u * 4u;
+    } else {
+        c.w[0] = c.w[1] = c.w[2] = c.w[3] = 1;
+    }
+    return c;
+}
+
+}  // namespace
+
+hipError_t launch_bc7enc_image(const Geometry &g, const gic_options &o, void *dst, hipStream_t s)
+{
+    const EncCfg cf = make_cfg(o);
+    const uint32_t wg = 256, grid = (g.total + wg - 1) / wg;
+    const int fa = o.force_alpha_one || g.channels < 4;
+    if (o.bc7enc_perceptual)
+        hipLaunchKernelGGL(bc7enc_image_kernel<true>, dim3(grid), dim3(wg), 0, s, g, cf, fa, (uint4 *)dst);
+    else
+        hipLaunchKernelGGL(bc7enc_image_kernel<false>, dim3(grid), dim3(wg), 0, s, g, cf, fa, (uint4 *)dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_bc7enc_blocks_u8(const uint32_t *blocks, uint32_t n, const gic_options &o, void *dst, hipStream_t s)
+{
+    const EncCfg cf = make_cfg(o);
+    const uint32_t wg = 256, grid = (n + wg - 1) / wg;
+    if (o.bc7enc_perceptual)
+        hipLaunchKernelGGL(bc7enc_blocks_kernel<true>, dim3(grid), dim3(wg), 0, s, (const uint4 *)blocks, n, cf,
+                           (uint4 *)dst);
+    else
+        hipLaunchKernelGGL(bc7enc_blocks_kernel<false>, dim3(grid), dim3(wg), 0, s, (const uint4 *)blocks, n, cf,
+                           (uint4 *)dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_bc7enc_blocks_f32(const float *blocks, uint32_t n, const gic_options &o, void *dst, hipStream_t s)
+{
+    const EncCfg cf = make_cfg(o);
+    const uint32_t wg = 256, grid = (n + wg - 1) / wg;
+    if (o.bc7enc_perceptual)
+        hipLaunchKernelGGL(bc7enc_f32_kernel<true>, dim3(grid), dim3(wg), 0, s, blocks, n, cf, (uint4 *)dst);
+    else
+        hipLaunchKernelGGL(bc7enc_f32_kernel<false>, dim3(grid), dim3(wg), 0, s, blocks, n, cf, (uint4 *)dst);
+    return hipGetLastError();
+}
+
+}  // namespace gic

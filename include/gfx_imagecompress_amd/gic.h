@@ -33,7 +33,9 @@ typedef enum gic_format {
     GIC_FMT_BC3 = 3, /* BC4-style alpha (:125) + 4-colour RGB half (amd_bc3_compressor.cpp:41-46) */
     GIC_FMT_BC4 = 4, /* Image_CompressAMDAlphaSingleModeBlock on one channel (:125) */
     GIC_FMT_BC5 = 5, /* two BC4 blocks, channel 0 then channel 1 (amd_bc5_compressor.cpp:35-41) */
-    GIC_FMT_BC7 = 7  /* BC7BlockEncoder::CompressBlock (amd_bc7_body.cpp:1289) */
+    GIC_FMT_BC7 = 7, /* BC7BlockEncoder::CompressBlock (amd_bc7_body.cpp:1289) */
+    GIC_FMT_BC7ENC16 = 8 /* BC7 blocks (modes 1/6) by bc7enc16, the reference's fast BC7 encoder
+                            (richgel999_bc7enc16.cpp:1517, Image_CompressRichGel999BC7 :21) */
 } gic_format;
 
 /* Texel encodings of a source image (what Image_GetPixelAtF decodes). */
@@ -62,6 +64,15 @@ typedef struct gic_options {
     uint32_t bc7_shake_ranks;    /* partitions shaken per single-index BC7 mode: 0 = the reference's
                                     count (8 at quality 1, bit-exact search); 1..8 caps it (pruned
                                     search, held to the per-block MSE tolerance) */
+    /* bc7enc16 (GIC_FMT_BC7ENC16) settings, bc7enc16_compress_block_params
+     * (richgel999_bc7enc16.h:17-36); defaults are the image API's
+     * (Image_CompressDefaultRichGel99Options :13-19: perceptual, fast = false
+     * -> uber level 4, Image_CompressRichGel999BC7enc16 :73-97) */
+    uint8_t bc7enc_perceptual;      /* 1: YCbCr-weighted error, weights 128/64/16/32 (default 1) */
+    uint8_t bc7enc_uber_level;      /* 0..4 (default 4; fast = true gives 0) */
+    uint8_t bc7enc_max_partitions;  /* mode-1 partitions scanned, 0..64 (default 64) */
+    uint8_t bc7enc_least_squares;   /* m_try_least_squares (default 1) */
+    uint8_t bc7enc_filterbank;      /* m_mode1_partition_estimation_filterbank (default 1) */
 } gic_options;
 
 void gic_default_options(gic_options *opt);
@@ -102,10 +113,18 @@ int gic_hip_encode_rows_src(gic_format fmt, gic_source src_type, const void *d_s
 /* Block-level batch: n blocks of 16 texels, float in [0,1].
  *   BC1/BC2/BC3/BC7: d_blocks holds n x 64 floats (RGBA per texel, texel-major).
  *   BC4:     d_blocks holds n x 16 floats.
+ *   BC7ENC16: n x 64 floats, each texel to RGBA8 as saturate(v) * 255 + 0.5.
  * This is the batched form of the reference's block API
  * (imagecompress.h:111-136). */
 int gic_hip_encode_blocks_f32(gic_format fmt, const float *d_blocks, uint32_t n, const gic_options *opt,
                               uint8_t *d_dst, double *d_block_err, void *stream);
+
+/* bc7enc16 at its block ABI (Image_CompressRichGel999BC7enc16,
+ * richgel999_bc7enc16.cpp:73): n blocks of 16 packed RGBA8 texels
+ * (R | G << 8 | B << 16 | A << 24, texel-major), 16-byte BC7 blocks out.
+ * fmt must be GIC_FMT_BC7ENC16. */
+int gic_hip_encode_blocks_u8(gic_format fmt, const uint32_t *d_blocks, uint32_t n, const gic_options *opt,
+                             uint8_t *d_dst, void *stream);
 
 /* Decode BCn blocks resident in HBM (row-major per slice, slices stacked, as
  * the encoders write them) to RGBA8: d_rgba receives slices x height rows of

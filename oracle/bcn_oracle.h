@@ -75,6 +75,13 @@ int orc_encode_image_bc7_ex(const uint8_t *src, uint32_t width, uint32_t height,
                             int32_t first_row, int32_t num_rows, int threads, float quality, uint8_t mode_mask,
                             int shake_ranks, uint8_t *dst, double *block_err);
 
+/* bc7enc16, the reference's fast BC7 encoder (richgel999_bc7enc16.cpp):
+ * Image_CompressRichGel999BC7enc16 on one packed RGBA8 block (:73-97) and the
+ * Image_CompressRichGel999BC7 block loop over an 8-bit image (:21-71). */
+void orc_bc7enc_block(const uint8_t rgba[64], int fast, int perceptual, uint8_t out[16]);
+int orc_encode_image_bc7enc(const uint8_t *src, uint32_t width, uint32_t height, uint32_t slices, uint32_t channels,
+                            int fast, int perceptual, uint8_t *dst);
+
 /* helpers exposed for unit tests */
 void orc_load_block_rgba8(const uint8_t *src, uint32_t width, uint32_t height,
                           uint32_t channels, uint32_t bx, uint32_t by,

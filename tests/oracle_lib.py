@@ -55,6 +55,10 @@ def lib() -> ctypes.CDLL:
         _lib.orc_bc7_shake_ramp.restype = ctypes.c_int
         _lib.orc_bc7_decode.argtypes = [vp, vp]
         _lib.orc_bc7_decode_n.argtypes = [vp, ctypes.c_size_t, vp]
+        _lib.orc_bc7enc_block.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
+        _lib.orc_encode_image_bc7enc.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                 ctypes.c_uint32, ctypes.c_int, ctypes.c_int, vp]
+        _lib.orc_encode_image_bc7enc.restype = ctypes.c_int
     return _lib
 
 
@@ -139,6 +143,29 @@ def bc7_block(block: np.ndarray, mode_mask: int = 0xFF):
     out = np.zeros(16, np.uint8)
     e = lib().orc_bc7_block(b.ctypes.data, mode_mask, 1, 1.0, 1, 1, 1.0, out.ctypes.data)
     return out.tobytes(), e
+
+
+def encode_image_bc7enc(img: np.ndarray, fast: bool = False, perceptual: bool = True) -> np.ndarray:
+    """bc7enc16 over an 8-bit image (Image_CompressRichGel999BC7's block loop)."""
+    a = np.ascontiguousarray(img, dtype=np.uint8)
+    if a.ndim == 2:
+        a = a[:, :, None]
+    if a.ndim == 3:
+        a = a[None]
+    s, h, w, c = a.shape
+    out = np.zeros((s * ((h + 3) // 4) * ((w + 3) // 4), 16), np.uint8)
+    if lib().orc_encode_image_bc7enc(a.ctypes.data, w, h, s, c, int(fast), int(perceptual), out.ctypes.data) != 0:
+        raise RuntimeError("oracle bc7enc16 encode failed")
+    return out
+
+
+def bc7enc_blocks(rgba: np.ndarray, fast: bool = False, perceptual: bool = True) -> np.ndarray:
+    """bc7enc16 on (n, 16, 4) uint8 blocks (Image_CompressRichGel999BC7enc16)."""
+    b = np.ascontiguousarray(rgba, dtype=np.uint8).reshape(-1, 64)
+    out = np.zeros((b.shape[0], 16), np.uint8)
+    for i in range(b.shape[0]):
+        lib().orc_bc7enc_block(b[i].ctypes.data, int(fast), int(perceptual), out[i].ctypes.data)
+    return out
 
 
 def bc7_decode(blocks: np.ndarray) -> np.ndarray:

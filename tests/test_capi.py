@@ -47,6 +47,11 @@ def test_default_options_match_reference():
     assert abs(o.bc1_alpha_threshold - 128 / 255.0) < 1e-7
     assert o.refinement_steps == 1 and o.bc4_channel == 1 and o.bc7_mode_mask == 0xFF
     assert o.colour_restrict == 1 and o.alpha_restrict == 1 and o.bc7_quality == 1.0
+    # bc7enc16: Image_CompressDefaultRichGel99Options {perceptual = true, fast = false} (richgel999_bc7enc16.cpp:13-19)
+    assert (o.bc7enc_perceptual, o.bc7enc_uber_level, o.bc7enc_max_partitions) == (1, 4, 64)
+    assert o.bc7enc_least_squares == 1 and o.bc7enc_filterbank == 1
+    py = gic.Options().to_c()
+    assert bytes(py) == bytes(o), "Python Options defaults drift from gic_default_options"
 
 
 def test_block_bytes_and_argument_checks():
@@ -57,6 +62,11 @@ def test_block_bytes_and_argument_checks():
     assert lib.gic_hip_encode(1, None, 4, 4, 1, 4, 16, None, None, None, None) == gic.GIC_EINVAL
     o = gic.Options(adaptive_weights=True).to_c()
     assert lib.gic_hip_encode(1, 16, 4, 4, 1, 4, 16, ctypes.byref(o), 16, None, None) == gic.GIC_EUNSUP
+    assert lib.gic_block_bytes(gic.FMT_BC7ENC16) == 16
+    o = gic.Options(bc7enc_uber_level=5).to_c()
+    assert lib.gic_hip_encode(gic.FMT_BC7ENC16, 16, 4, 4, 1, 4, 16, ctypes.byref(o), 16, None, None) == gic.GIC_EINVAL
+    assert lib.gic_hip_encode_blocks_u8(gic.FMT_BC7, 16, 1, None, 16, None) == gic.GIC_EINVAL
+    assert lib.gic_hip_encode_blocks_u8(gic.FMT_BC7ENC16, None, 1, None, 16, None) == gic.GIC_EINVAL
 
 
 def test_image_model_and_pick_type():
