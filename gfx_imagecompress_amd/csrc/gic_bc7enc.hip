@@ -44,11 +44,27 @@ __device__ __forceinline__ float sat(float v) { return clampf_r(v, 0.f, 1.0f); }
 __device__ __forceinline__ int clampi_r(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 __device__ __forceinline__ uint32_t sel_at(uint64_t s, int i) { return (uint32_t)(s >> (4 * i)) & 15u; }
 
+// A texel word the optimiser must treat as new at every use: without it the
+// per-texel channel values and their float conversions (16 x 4 each) are hoisted
+// out of the trial loops and held live, which spills the kernel.
+__device__ __forceinline__ uint32_t tex(const uint32_t px[16], int i)
+{
+    uint32_t v = px[i];
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
 // g_bc7_weights3/4 (:130-131): round(64 s / (N - 1))
 __device__ __forceinline__ uint32_t bc7w(uint32_t s, uint32_t N)
 {
     return N == 16 ? (s * 64u + 7u) / 15u : (s * 64u + 3u) / 7u;
 }
+
+// 24-bit multiplies (full rate).  Every factor below is a channel difference
+// |d| <= 946 or a weight times one (<= 512 * 946 < 2^23), and every product and
+// sum stays below 2^31, so these equal the reference's uint32 arithmetic.
+__device__ __forceinline__ int mul24(int a, int b) { return __mul24(a, b); }
+__device__ __forceinline__ int mad24(int a, int b, int c) { return __mul24(a, b) + c; }
 
 // interpolated channel k of the ramp point with weight w (:445, :1053)
 __device__ __forceinline__ int lerp_ch(uint32_t a, uint32_t b, int k, uint32_t w)
@@ -89,18 +105,6 @@ __device__ __forceinline__ uint32_t expand(uint32_t q, uint32_t n)
     return r;
 }
 
-// compute_color_distance_rgb / _rgba with perceptual = false (:325-355)
-__device__ __forceinline__ uint32_t lin_err(int r, int g, int b, int a, uint32_t c, bool alpha, const EncCfg &cf)
-{
-    const int dr = r - (int)ch(c, 0), dg = g - (int)ch(c, 1), db = b - (int)ch(c, 2);
-    uint32_t e = cf.w[0] * (uint32_t)(dr * dr) + cf.w[1] * (uint32_t)(dg * dg) + cf.w[2] * (uint32_t)(db * db);
-    if (alpha) {
-        const int da = a - (int)ch(c, 3);
-        e += cf.w[3] * (uint32_t)(da * da);
-    }
-    return e;
-}
-
 // the YCbCr-style transform of compute_color_distance_rgb (:331-339)
 __device__ __forceinline__ void ycc(int r, int g, int b, int &l, int &cr, int &cb)
 {
@@ -109,30 +113,25 @@ __device__ __forceinline__ void ycc(int r, int g, int b, int &l, int &cr, int &c
     cb = (b << 9) - l;
 }
 
-template <bool P>
-__device__ __forceinline__ uint32_t pair_err(int l1, int cr1, int cb1, int a1, int l2, int cr2, int cb2, int a2,
-                                             int r1, int g1, int b1, int r2, int g2, int b2, bool alpha,
-                                             const EncCfg &cf)
+// weighted squared distance w0 d0^2 + w1 d1^2 + w2 d2^2 [+ e]
+__device__ __forceinline__ uint32_t wsq(int d0, int d1, int d2, const EncCfg &cf, int e = 0)
 {
-    int d0, d1, d2;
-    if (P) {
-        d0 = (l1 - l2) >> 8;
-        d1 = (cr1 - cr2) >> 8;
-        d2 = (cb1 - cb2) >> 8;
-    } else {
-        d0 = r1 - r2;
-        d1 = g1 - g2;
-        d2 = b1 - b2;
-    }
-    uint32_t e = cf.w[0] * (uint32_t)(d0 * d0) + cf.w[1] * (uint32_t)(d1 * d1) + cf.w[2] * (uint32_t)(d2 * d2);
-    if (alpha) e += cf.w[3] * (uint32_t)((a1 - a2) * (a1 - a2));
-    return e;
+    return (uint32_t)e + __umul24(cf.w[0], (uint32_t)__mul24(d0, d0)) + __umul24(cf.w[1], (uint32_t)__mul24(d1, d1)) +
+           __umul24(cf.w[2], (uint32_t)__mul24(d2, d2));
 }
 
-// evaluate_solution :405-572
+// compute_color_distance_rgb with perceptual = true, from the two colours' transforms
+__device__ __forceinline__ uint32_t ycc_err(int l1, int cr1, int cb1, int l2, int cr2, int cb2, const EncCfg &cf,
+                                            int e = 0)
+{
+    return wsq((l1 - l2) >> 8, (cr1 - cr2) >> 8, (cb1 - cb2) >> 8, cf, e);
+}
+
+// evaluate_solution :405-572.  Masked-out texels are computed and discarded
+// (branch-free); the integer totals do not depend on summation order.
 template <bool P>
-__device__ void evaluate(uint32_t lo, uint32_t hi, uint32_t pb0, uint32_t pb1, const Prob &pr, const uint32_t px[16], const Ycc &tx,
-                         const EncCfg &cf, Res &r)
+__device__ __forceinline__ void evaluate(uint32_t lo, uint32_t hi, uint32_t pb0, uint32_t pb1, const Prob &pr, const uint32_t px[16],
+                         const Ycc &tx, const EncCfg &cf, Res &r)
 {
     const uint32_t p1 = pr.mode1 ? pb0 : pb1;
     uint32_t qlo = 0, qhi = 0;
@@ -145,6 +144,8 @@ __device__ void evaluate(uint32_t lo, uint32_t hi, uint32_t pb0, uint32_t pb1, c
     const uint32_t N = pr.nsel;
     uint32_t tot = 0;
     uint64_t ts = 0;
+    const bool any_alpha = __any(pr.alpha);
+    const int w3 = pr.alpha ? (int)cf.w[3] : 0;
     if (!P) {
         const int ar = ch(a, 0), ag = ch(a, 1), ab = ch(a, 2), aa = ch(a, 3);
         const int dr = (int)ch(b, 0) - ar, dg = (int)ch(b, 1) - ag, db = (int)ch(b, 2) - ab;
@@ -152,52 +153,63 @@ __device__ void evaluate(uint32_t lo, uint32_t hi, uint32_t pb0, uint32_t pb1, c
         const float f = N / (float)(dr * dr + dg * dg + db * db + da * da + .00000125f);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            if (!((pr.mask >> i) & 1u)) continue;
-            const uint32_t c = px[i];
-            int dot = ((int)ch(c, 0) - ar) * dr + ((int)ch(c, 1) - ag) * dg + ((int)ch(c, 2) - ab) * db;
-            if (pr.alpha) dot += ((int)ch(c, 3) - aa) * da;
+            const uint32_t c = tex(px, i);
+            const int cr = ch(c, 0), cg = ch(c, 1), cb = ch(c, 2), ca = ch(c, 3);
+            int dot = (cr - ar) * dr + (cg - ag) * dg + (cb - ab) * db;
+            if (pr.alpha) dot += (ca - aa) * da;
             int s = (int)((float)dot * f + .5f);
             s = clampi_r(s, 1, (int)N - 1);
             const uint32_t w0 = bc7w(s - 1, N), w1 = bc7w(s, N);
-            const uint32_t e0 = lin_err(lerp_ch(a, b, 0, w0), lerp_ch(a, b, 1, w0), lerp_ch(a, b, 2, w0),
-                                        lerp_ch(a, b, 3, w0), c, pr.alpha, cf);
-            const uint32_t e1 = lin_err(lerp_ch(a, b, 0, w1), lerp_ch(a, b, 1, w1), lerp_ch(a, b, 2, w1),
-                                        lerp_ch(a, b, 3, w1), c, pr.alpha, cf);
-            // both reference branches move down exactly when err0 < err1 (:479, :508)
-            if (e0 < e1) {
-                tot += e0;
-                --s;
-            } else {
-                tot += e1;
+            int ea0 = 0, ea1 = 0;
+            if (any_alpha) {   // wave-uniform: skipped by waves of opaque blocks
+                const int d0 = lerp_ch(a, b, 3, w0) - ca, d1 = lerp_ch(a, b, 3, w1) - ca;
+                ea0 = mad24(mul24(w3, d0), d0, 0);
+                ea1 = mad24(mul24(w3, d1), d1, 0);
             }
-            ts |= (uint64_t)s << (4 * i);
+            const uint32_t e0 =
+                wsq(lerp_ch(a, b, 0, w0) - cr, lerp_ch(a, b, 1, w0) - cg, lerp_ch(a, b, 2, w0) - cb, cf, ea0);
+            const uint32_t e1 =
+                wsq(lerp_ch(a, b, 0, w1) - cr, lerp_ch(a, b, 1, w1) - cg, lerp_ch(a, b, 2, w1) - cb, cf, ea1);
+            // both reference branches move down exactly when err0 < err1 (:479, :508)
+            const bool down = e0 < e1;
+            const bool in = (pr.mask >> i) & 1u;
+            tot += in ? (down ? e0 : e1) : 0u;
+            ts |= (uint64_t)(in ? (uint32_t)(s - down) : 0u) << (4 * i);
         }
     } else {
-        // ramp point outer (a real loop), texels inner: each texel keeps its first
-        // minimum as the reference's per-texel scan does (:522-555)
-        uint32_t be[16];
+        // ramp point outer (a real loop), texels inner.  Each texel keeps the
+        // minimum of (error << 4 | selector): the least error, first selector on
+        // ties -- the reference's strict-< scan (:522-555); errors are < 2^28.
+        uint32_t key[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) be[i] = kNone;
+        for (int i = 0; i < 16; ++i) key[i] = kNone;
 #pragma unroll 1
         for (uint32_t j = 0; j < N; ++j) {
             const uint32_t w = bc7w(j, N);
             int l1, cr1, cb1;
             ycc(lerp_ch(a, b, 0, w), lerp_ch(a, b, 1, w), lerp_ch(a, b, 2, w), l1, cr1, cb1);
             const int a1 = lerp_ch(a, b, 3, w);
+            if (any_alpha) {   // wave-uniform
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                if (!((pr.mask >> i) & 1u)) continue;
-                const uint32_t e = pair_err<true>(l1, cr1, cb1, a1, tx.l[i], tx.cr[i], tx.cb[i], (int)ch(px[i], 3), 0,
-                                                  0, 0, 0, 0, 0, pr.alpha, cf);
-                if (e < be[i]) {
-                    be[i] = e;
-                    ts = (ts & ~((uint64_t)15u << (4 * i))) | ((uint64_t)j << (4 * i));
+                for (int i = 0; i < 16; ++i) {
+                    const int d = a1 - (int)ch(tex(px, i), 3);
+                    const uint32_t e = ycc_err(l1, cr1, cb1, tx.l[i], tx.cr[i], tx.cb[i], cf, mad24(mul24(w3, d), d, 0));
+                    key[i] = min(key[i], (e << 4) | j);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const uint32_t e = ycc_err(l1, cr1, cb1, tx.l[i], tx.cr[i], tx.cb[i], cf);
+                    key[i] = min(key[i], (e << 4) | j);
                 }
             }
         }
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
-            if ((pr.mask >> i) & 1u) tot += be[i];
+        for (int i = 0; i < 16; ++i) {
+            const bool in = (pr.mask >> i) & 1u;
+            tot += in ? key[i] >> 4 : 0u;
+            ts |= (uint64_t)(in ? key[i] & 15u : 0u) << (4 * i);
+        }
     }
     if (tot < r.err) {
         r.err = tot;
@@ -212,7 +224,7 @@ __device__ void evaluate(uint32_t lo, uint32_t hi, uint32_t pb0, uint32_t pb1, c
 // find_optimal_solution :606-729 (modes 1 and 6 both carry p-bits) with
 // fixDegenerateEndpoints :574-604 (mode 1)
 template <bool P>
-__device__ void fit(float xl[4], float xh[4], const Prob &pr, const uint32_t px[16], const Ycc &tx, const EncCfg &cf, Res &r)
+__device__ __forceinline__ void fit(float xl[4], float xh[4], const Prob &pr, const uint32_t px[16], const Ycc &tx, const EncCfg &cf, Res &r)
 {
 #pragma unroll
     for (int k = 0; k < 4; ++k) xl[k] = sat(xl[k]), xh[k] = sat(xh[k]);
@@ -290,24 +302,24 @@ __device__ void fit(float xl[4], float xh[4], const Prob &pr, const uint32_t px[
 }
 
 // compute_least_squares_endpoints_rgb / _rgba :197-280, then the 1/255 scale
-__device__ void lsq(const Prob &pr, uint64_t sel, const uint32_t px[16], const EncLds &L, float xl[4], float xh[4])
+__device__ __forceinline__ void lsq(const Prob &pr, uint64_t sel, const uint32_t px[16], const EncLds &L, float xl[4], float xh[4])
 {
     const float *wx = L.wx + (pr.nsel == 16 ? 32 : 0);
     float z00 = 0.0f, z10 = 0.0f, z11 = 0.0f;
     float q00[4] = {0.f, 0.f, 0.f, 0.f}, t[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        if (!((pr.mask >> i) & 1u)) continue;
+    for (int i = 0; i < 16; ++i) {   // texel order; texels outside the subset leave every sum as it is
+        const bool in = (pr.mask >> i) & 1u;
         const float *w4 = wx + 4 * sel_at(sel, i);
-        z00 += w4[0];
-        z10 += w4[1];
-        z11 += w4[2];
+        z00 = in ? z00 + w4[0] : z00;
+        z10 = in ? z10 + w4[1] : z10;
+        z11 = in ? z11 + w4[2] : z11;
         const float w = w4[3];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const float c = (float)ch(px[i], k);
-            q00[k] += w * c;
-            t[k] += c;
+            const float c = (float)ch(tex(px, i), k);
+            q00[k] = in ? q00[k] + w * c : q00[k];
+            t[k] = in ? t[k] + c : t[k];
         }
     }
     const float z01 = z10;
@@ -326,7 +338,7 @@ __device__ void lsq(const Prob &pr, uint64_t sel, const uint32_t px[16], const E
 
 // pack_mode1_to_one_color :357-403
 template <bool P>
-__device__ void one_colour(uint32_t cr, uint32_t cg, uint32_t cb, const Prob &pr, const uint32_t px[16], const Ycc &tx,
+__device__ __forceinline__ void one_colour(uint32_t cr, uint32_t cg, uint32_t cb, const Prob &pr, const uint32_t px[16], const Ycc &tx,
                            const EncCfg &cf, const EncLds &L, Res &r)
 {
     uint32_t best = kNone, bp = 0;
@@ -355,10 +367,12 @@ __device__ void one_colour(uint32_t cr, uint32_t cg, uint32_t cb, const Prob &pr
     uint64_t ts = 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        if (!((pr.mask >> i) & 1u)) continue;
-        const uint32_t c = px[i];
-        tot += pair_err<P>(ql, qcr, qcb, 0, tx.l[i], tx.cr[i], tx.cb[i], 0, q[0], q[1], q[2], ch(c, 0), ch(c, 1), ch(c, 2), false, cf);
-        ts |= (uint64_t)2u << (4 * i);
+        const uint32_t c = tex(px, i);
+        const uint32_t e = P ? ycc_err(ql, qcr, qcb, tx.l[i], tx.cr[i], tx.cb[i], cf)
+                             : wsq(q[0] - (int)ch(c, 0), q[1] - (int)ch(c, 1), q[2] - (int)ch(c, 2), cf);
+        const bool in = (pr.mask >> i) & 1u;
+        tot += in ? e : 0u;
+        ts |= (uint64_t)(in ? 2u : 0u) << (4 * i);
     }
     r.sel = ts;
     r.err = tot;
@@ -366,7 +380,7 @@ __device__ void one_colour(uint32_t cr, uint32_t cg, uint32_t cb, const Prob &pr
 
 // color_cell_compression :731-1024
 template <bool P>
-__device__ Res cell(const Prob &pr, const uint32_t px[16], const Ycc &tx, const EncCfg &cf, const EncLds &L)
+__device__ __forceinline__ Res cell(const Prob &pr, const uint32_t px[16], const Ycc &tx, const EncCfg &cf, const EncLds &L)
 {
     Res r;
     r.err = kNone;
@@ -374,13 +388,11 @@ __device__ Res cell(const Prob &pr, const uint32_t px[16], const Ycc &tx, const 
     r.sel = 0;
     if (pr.mode1) {   // the subset is one colour: pack it directly (:738-754)
         uint32_t first = 0;
-        bool seen = false, same = true;
+        bool same = true;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            if (!((pr.mask >> i) & 1u)) continue;
-            if (!seen) first = px[i] & 0xffffffu, seen = true;
-            same = same && (px[i] & 0xffffffu) == first;
-        }
+        for (int i = 15; i >= 0; --i) first = ((pr.mask >> i) & 1u) ? tex(px, i) & 0xffffffu : first;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) same = same && (!((pr.mask >> i) & 1u) || (tex(px, i) & 0xffffffu) == first);
         if (same) {
             one_colour<P>(ch(first, 0), ch(first, 1), ch(first, 2), pr, px, tx, cf, L, r);
             return r;
@@ -390,26 +402,23 @@ __device__ Res cell(const Prob &pr, const uint32_t px[16], const Ycc &tx, const 
     float m[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        if (!((pr.mask >> i) & 1u)) continue;
+        const bool in = (pr.mask >> i) & 1u;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) m[k] = m[k] + (float)ch(px[i], k);
+        for (int k = 0; k < 4; ++k) m[k] = in ? m[k] + (float)ch(tex(px, i), k) : m[k];
     }
     float ms[4], mn[4], ax[4] = {0.f, 0.f, 0.f, 0.f};
     const float inv_n = 1.0f / (float)pr.n, inv_n255 = 1.0f / (float)(pr.n * 255.0f);
 #pragma unroll
     for (int k = 0; k < 4; ++k) ms[k] = m[k] * inv_n, mn[k] = sat(m[k] * inv_n255);
-    if (pr.alpha) {   // incremental PCA (:773-790)
-        bool seen = false;
+    if (pr.alpha) {   // incremental PCA (:773-790); alpha problems are whole blocks (mode 6)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            if (!((pr.mask >> i) & 1u)) continue;
             float c[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) c[k] = (float)ch(px[i], k) - ms[k];
+            for (int k = 0; k < 4; ++k) c[k] = (float)ch(tex(px, i), k) - ms[k];
             float n[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) n[k] = seen ? ax[k] : c[k];
-            seen = true;
+            for (int k = 0; k < 4; ++k) n[k] = i ? ax[k] : c[k];
             float s = n[0] * n[0] + n[1] * n[1] + n[2] * n[2] + n[3] * n[3];
             if (s != 0.0f) {
                 s = 1.0f / sqrtf(s);
@@ -435,9 +444,11 @@ __device__ Res cell(const Prob &pr, const uint32_t px[16], const Ycc &tx, const 
         float cv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            if (!((pr.mask >> i) & 1u)) continue;
-            const float r0 = (int)ch(px[i], 0) - ms[0], g0 = (int)ch(px[i], 1) - ms[1], b0 = (int)ch(px[i], 2) - ms[2];
-            cv[0] += r0 * r0, cv[1] += r0 * g0, cv[2] += r0 * b0, cv[3] += g0 * g0, cv[4] += g0 * b0, cv[5] += b0 * b0;
+            const bool in = (pr.mask >> i) & 1u;
+            const float r0 = (int)ch(tex(px, i), 0) - ms[0], g0 = (int)ch(tex(px, i), 1) - ms[1], b0 = (int)ch(tex(px, i), 2) - ms[2];
+            const float t[6] = {r0 * r0, r0 * g0, r0 * b0, g0 * g0, g0 * b0, b0 * b0};
+#pragma unroll
+            for (int k = 0; k < 6; ++k) cv[k] = in ? cv[k] + t[k] : cv[k];
         }
         float vr = .9f, vg = 1.0f, vb = .7f;
 #pragma unroll
@@ -475,13 +486,13 @@ __device__ Res cell(const Prob &pr, const uint32_t px[16], const Ycc &tx, const 
     float lo = 1e+9f, hi = -1e+9f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        if (!((pr.mask >> i) & 1u)) continue;
+        const bool in = (pr.mask >> i) & 1u;
         float q[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) q[k] = (float)ch(px[i], k) - ms[k];
+        for (int k = 0; k < 4; ++k) q[k] = (float)ch(tex(px, i), k) - ms[k];
         const float d = q[0] * ax[0] + q[1] * ax[1] + q[2] * ax[2] + q[3] * ax[3];
-        lo = lo < d ? lo : d;
-        hi = hi > d ? hi : d;
+        lo = (in && !(lo < d)) ? d : lo;
+        hi = (in && !(hi > d)) ? d : hi;
     }
     lo *= (1.0f / 255.0f);
     hi *= (1.0f / 255.0f);
@@ -519,10 +530,10 @@ __device__ Res cell(const Prob &pr, const uint32_t px[16], const Ycc &tx, const 
             smin = 16, smax = 0;
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                if (!((pr.mask >> i) & 1u)) continue;
+                const bool in = (pr.mask >> i) & 1u;
                 const uint32_t s = sel_at(base, i);
-                smin = s < smin ? s : smin;
-                smax = s > smax ? s : smax;
+                smin = in && s < smin ? s : smin;
+                smax = in && s > smax ? s : smax;
             }
         }
         if (t == 1 + nls + nub) grid = r.err > ((pr.n * 56u) >> 4);
@@ -536,10 +547,10 @@ __device__ Res cell(const Prob &pr, const uint32_t px[16], const Ycc &tx, const 
             if (t <= nls) {
                 ts = r.sel;
             } else if (t < 1 + nls + nub) {
+                // texels outside the subset get some selector in 0..15 that lsq ignores
                 const int u = t - 1 - nls;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    if (!((pr.mask >> i) & 1u)) continue;
                     uint32_t s = sel_at(base, i);
                     if (u != 1 && s == smin && s < pr.nsel - 1)
                         s++;
@@ -553,7 +564,6 @@ __device__ Res cell(const Prob &pr, const uint32_t px[16], const Ycc &tx, const 
                 const int ly = -Q + g / (Q + 2), hy = maxs - 1 + g % (Q + 2);
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    if (!((pr.mask >> i) & 1u)) continue;
                     const float v = floorf((float)maxs * ((float)sel_at(base, i) - (float)ly) / ((float)hy - (float)ly) +
                                            .5f);
                     ts |= (uint64_t)(uint32_t)clampf_r(v, 0, (float)maxs) << (4 * i);
@@ -573,52 +583,79 @@ __device__ Res cell(const Prob &pr, const uint32_t px[16], const Ycc &tx, const 
     return r;
 }
 
-// color_cell_compression_est :1026-1162 for the texels of `mask` (full sums:
-// the reference's partial-sum exits only ever make a candidate lose a '<' test)
-template <bool P>
-__device__ uint32_t estimate(uint32_t mask, const uint32_t px[16], const Ycc &tx, const EncCfg &cf)
+// color_cell_compression_est :1026-1162 for both subsets of a two-subset shape
+// in one pass (m0 = the texels of subset 0): bounding-box endpoints, 8 ramp
+// points, selectors by dot-product thresholds.  The reference stops a sum once
+// it exceeds the best so far; its caller only compares with '<', so full sums
+// are equivalent.
+struct EstSubset {
+    int lo[3], hi[3], a[3], th[7];
+};
+
+__device__ __forceinline__ void est_setup(EstSubset &e)
 {
-    int lo[3] = {255, 255, 255}, hi[3] = {0, 0, 0};
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        if (!((mask >> i) & 1u)) continue;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int v = ch(px[i], k);
-            lo[k] = v < lo[k] ? v : lo[k];
-            hi[k] = v > hi[k] ? v : hi[k];
-        }
-    }
-    const int ar = hi[0] - lo[0], ag = hi[1] - lo[1], ab = hi[2] - lo[2];
-    int th[7], prev = lo[0] * ar + lo[1] * ag + lo[2] * ab;
+    for (int k = 0; k < 3; ++k) e.a[k] = e.hi[k] - e.lo[k];
+    int prev = e.lo[0] * e.a[0] + e.lo[1] * e.a[1] + e.lo[2] * e.a[2];
 #pragma unroll
     for (int s = 1; s < 8; ++s) {
         const int w = (int)bc7w((uint32_t)s, 8);
-        const int r = (lo[0] * (64 - w) + hi[0] * w + 32) >> 6, g = (lo[1] * (64 - w) + hi[1] * w + 32) >> 6,
-                  b = (lo[2] * (64 - w) + hi[2] * w + 32) >> 6;
-        const int d = r * ar + g * ag + b * ab;
-        th[s - 1] = (prev + d + 1) >> 1;
+        int d = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) d += ((e.lo[k] * (64 - w) + e.hi[k] * w + 32) >> 6) * e.a[k];
+        e.th[s - 1] = (prev + d + 1) >> 1;
         prev = d;
     }
+}
+
+template <bool P>
+__device__ __forceinline__ uint32_t estimate2(uint32_t m0, const uint32_t px[16], const Ycc &tx, const EncCfg &cf)
+{
+    EstSubset s0, s1;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) s0.lo[k] = s1.lo[k] = 255, s0.hi[k] = s1.hi[k] = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const bool in0 = (m0 >> i) & 1u;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int v = ch(tex(px, i), k);
+            s0.lo[k] = in0 && v < s0.lo[k] ? v : s0.lo[k];
+            s0.hi[k] = in0 && v > s0.hi[k] ? v : s0.hi[k];
+            s1.lo[k] = !in0 && v < s1.lo[k] ? v : s1.lo[k];
+            s1.hi[k] = !in0 && v > s1.hi[k] ? v : s1.hi[k];
+        }
+    }
+    est_setup(s0);
+    est_setup(s1);
     uint32_t tot = 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        if (!((mask >> i) & 1u)) continue;
-        const int cr = ch(px[i], 0), cg = ch(px[i], 1), cb = ch(px[i], 2);
-        const int d = ar * cr + ag * cg + ab * cb;
-        int s = 0;   // the dots of the ramp rise with s, so the first threshold from the top is a count
+        const bool in0 = (m0 >> i) & 1u;
+        int lo[3], hi[3], th[7];
+        int d = 0;
 #pragma unroll
-        for (int k = 0; k < 7; ++k) s += d >= th[k];
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = in0 ? s0.lo[k] : s1.lo[k];
+            hi[k] = in0 ? s0.hi[k] : s1.hi[k];
+            d += (in0 ? s0.a[k] : s1.a[k]) * (int)ch(tex(px, i), k);
+        }
+        int s = 0;   // the ramp's dots rise with s: the first threshold from the top is a count
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            th[k] = in0 ? s0.th[k] : s1.th[k];
+            s += d >= th[k];
+        }
         const int w = (int)bc7w((uint32_t)s, 8);
-        const int r = (lo[0] * (64 - w) + hi[0] * w + 32) >> 6, g = (lo[1] * (64 - w) + hi[1] * w + 32) >> 6,
-                  b = (lo[2] * (64 - w) + hi[2] * w + 32) >> 6;
+        int c[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) c[k] = (lo[k] * (64 - w) + hi[k] * w + 32) >> 6;
         if (P) {
             int l1, cr1, cb1;
-            ycc(r, g, b, l1, cr1, cb1);
-            tot += (uint32_t)(int)pair_err<true>(l1, cr1, cb1, 0, tx.l[i], tx.cr[i], tx.cb[i], 0, 0, 0, 0, 0, 0, 0,
-                                                 false, cf);
+            ycc(c[0], c[1], c[2], l1, cr1, cb1);
+            tot += ycc_err(l1, cr1, cb1, tx.l[i], tx.cr[i], tx.cb[i], cf);
         } else {
-            tot += pair_err<false>(0, 0, 0, 0, 0, 0, 0, 0, r, g, b, cr, cg, cb, false, cf);
+            tot += wsq(c[0] - (int)ch(tex(px, i), 0), c[1] - (int)ch(tex(px, i), 1), c[2] - (int)ch(tex(px, i), 2), cf);
         }
     }
     return tot;
@@ -634,7 +671,7 @@ __device__ __forceinline__ uint32_t shape_mask(uint32_t shape, uint32_t subset)
 
 // estimate_partition :1207-1281
 template <bool P>
-__device__ uint32_t pick_partition(const uint32_t px[16], const Ycc &tx, const EncCfg &cf)
+__device__ __forceinline__ uint32_t pick_partition(const uint32_t px[16], const Ycc &tx, const EncCfg &cf)
 {
     const uint32_t total = cf.max_parts < 64 ? cf.max_parts : 64;
     if (total <= 1) return 0;
@@ -648,7 +685,7 @@ __device__ uint32_t pick_partition(const uint32_t px[16], const Ycc &tx, const E
             continue;
         }
         const uint32_t m0 = shape_mask(kBc7Shape2[part], 0);
-        const uint32_t e = estimate<P>(m0, px, tx, cf) + estimate<P>(~m0 & 0xffffu, px, tx, cf);
+        const uint32_t e = estimate2<P>(m0, px, tx, cf);
         if (e < best) best = e, best_part = part;
         if (part == 34 && best_part != 34) stop = true;
         if (it == 13) key = best_part;
@@ -674,7 +711,7 @@ struct Bits {
 };
 
 // encode_bc7_block :1307-1388 for mode 6 (one subset) or mode 1 (partition `part`)
-__device__ uint4 pack_block(bool mode1, uint32_t part, uint64_t sel, const uint32_t lo[2], const uint32_t hi[2],
+__device__ __forceinline__ uint4 pack_block(bool mode1, uint32_t part, uint64_t sel, const uint32_t lo[2], const uint32_t hi[2],
                             uint32_t pb[2][2])
 {
     const uint32_t shape = mode1 ? kBc7Shape2[part] : 0u;
@@ -726,16 +763,16 @@ __device__ uint4 pack_block(bool mode1, uint32_t part, uint64_t sel, const uint3
 // :1390-1515 (m_endpoints_share_pbit, uninitialised for alpha blocks in the
 // reference, is false: mode 6 has a p-bit per endpoint)
 template <bool P>
-__device__ uint4 encode_block(const uint32_t px[16], const EncCfg &cf, const EncLds &L)
+__device__ __forceinline__ uint4 encode_block(const uint32_t px[16], const EncCfg &cf, const EncLds &L)
 {
     Ycc tx;
     if (P) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) ycc(ch(px[i], 0), ch(px[i], 1), ch(px[i], 2), tx.l[i], tx.cr[i], tx.cb[i]);
+        for (int i = 0; i < 16; ++i) ycc(ch(tex(px, i), 0), ch(tex(px, i), 1), ch(tex(px, i), 2), tx.l[i], tx.cr[i], tx.cb[i]);
     }
     bool alpha = false;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) alpha = alpha || (px[i] >> 24) < 255u;
+    for (int i = 0; i < 16; ++i) alpha = alpha || (tex(px, i) >> 24) < 255u;
     Res r6, s0, s1;
     s0.err = s1.err = kNone;
     bool mode1 = false;
@@ -791,7 +828,7 @@ __device__ __forceinline__ void load_tables(EncLds &L)
 // Image_CompressRichGel999BC7 :21-71 over 8-bit texels (its float round trip
 // v/255.0f -> R8G8B8A8_UNORM gives back the bytes)
 template <bool P>
-__global__ void __launch_bounds__(256) bc7enc_image_kernel(Geometry g, EncCfg cf, int force_alpha_one,
+__global__ void __launch_bounds__(256, 2) bc7enc_image_kernel(Geometry g, EncCfg cf, int force_alpha_one,
                                                            uint4 *__restrict__ dst)
 {
     __shared__ EncLds L;
@@ -807,7 +844,7 @@ __global__ void __launch_bounds__(256) bc7enc_image_kernel(Geometry g, EncCfg cf
 
 // Image_CompressRichGel999BC7enc16 :73-97: blocks of 16 packed RGBA8 words
 template <bool P>
-__global__ void __launch_bounds__(256) bc7enc_blocks_kernel(const uint4 *__restrict__ blocks, uint32_t n, EncCfg cf,
+__global__ void __launch_bounds__(256, 2) bc7enc_blocks_kernel(const uint4 *__restrict__ blocks, uint32_t n, EncCfg cf,
                                                             uint4 *__restrict__ dst)
 {
     __shared__ EncLds L;
@@ -827,7 +864,7 @@ __global__ void __launch_bounds__(256) bc7enc_blocks_kernel(const uint4 *__restr
 // to RGBA8 as saturate(v) * 255 + 0.5 truncated (TinyImageFormat's UNORM8 encode
 // is un-vendored; this rounding is unpinned and is the identity on v / 255.0f)
 template <bool P>
-__global__ void __launch_bounds__(256) bc7enc_f32_kernel(const float *__restrict__ blocks, uint32_t n, EncCfg cf,
+__global__ void __launch_bounds__(256, 2) bc7enc_f32_kernel(const float *__restrict__ blocks, uint32_t n, EncCfg cf,
                                                          uint4 *__restrict__ dst)
 {
     __shared__ EncLds L;
