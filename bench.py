@@ -67,6 +67,7 @@ def parse():
                    help="with the default BC1 workload, also time BC7 on this many block rows of the same "
                         "texture (-1 = the whole 8K texture, 0 = skip)")
     p.add_argument("--no-bc45", action="store_true", help="skip the BC4/BC5 8K legs (configs[2])")
+    p.add_argument("--no-bc7enc", action="store_true", help="skip the bc7enc16 (fast BC7 path) legs")
     p.add_argument("--bc7-shake-ranks", type=int, default=2,
                    help="pruned BC7 search leg: partitions shaken per single-index mode (gic_options."
                         "bc7_shake_ranks; 0 = skip the pruned leg).  The exact search (the reference's 8) is "
@@ -328,6 +329,50 @@ def bc45_leg(args, gic, fmt, world, dev, rank):
     return res
 
 
+def bc7enc16_leg(args, gic, src, size, world, dev, rank, fast):
+    """The reference's fast BC7 path (bc7enc16, Image_CompressRichGel999BC7,
+    richgel999_bc7enc16.cpp:21-71; ImageCompress_Compress(DXBC7, fast=true)) on
+    the same 8K G1 texture: steps x one launch over the rank's whole texture,
+    plus (rank 0) a bounded CPU-restatement sample with a bit-exactness check."""
+    import numpy as np
+    import torch
+    bx = by = (size + 3) // 4
+    dst = torch.empty(bx * by * 16, dtype=torch.uint8, device=dev)
+    opts = gic.Options.bc7enc16(fast=fast, perceptual=True)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        gic.encode_device(gic.FMT_BC7ENC16, src, size, size, 1, 4, dst, opts, 0, by, stream=stream)
+    for _ in range(max(1, args.warmup)):
+        step()
+    wall, kern_ms = _timed(world, dev, stream, step, args.steps)
+    alg = ALG_BYTES[7] * bx * by
+    res = {"metric": f"Mpixels/s BC7 by bc7enc16 (the reference's fast BC7 path), perceptual, "
+                     f"uber level {0 if fast else 4} ({'fast = true' if fast else 'image-API default'})",
+           "value": round(size * size * world * args.steps / wall / 1e6, 3), "unit": "Mpixels/s",
+           "blocks_per_s": round(bx * by * world * args.steps / wall, 1),
+           "ms_per_step": round(wall / args.steps * 1e3, 4), "kernel_ms": round(kern_ms, 4), "dtype": "f32+int32",
+           "roofline": {"bound": "valu", "achieved": round(alg / (kern_ms * 1e-3) / 1e9, 3), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(alg / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
+                        "alg_bytes_per_launch": alg}}
+    if rank == 0 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        host = src.cpu().numpy()[0]
+        threads = _cpu_threads()
+        rows = 4 if not fast else 16
+        c0 = time.perf_counter()
+        ref = oracle_lib.encode_image_bc7enc_rows(host, 0, rows, threads=threads, fast=fast, perceptual=True)
+        dt = time.perf_counter() - c0
+        got = dst.cpu().numpy().reshape(-1, 16)[:rows * bx]
+        res["cpu_baseline"] = {"value": round(rows * 4 * size / dt / 1e6, 4), "unit": "Mpixels/s", "cores": threads,
+                               "kind": "port", "cpu_model": cpu_model(),
+                               "sample": f"block rows 0-{rows - 1} ({rows * bx} blocks, {dt:.2f} s, {threads} threads)"}
+        res["gpu_parity"] = "bit-exact" if np.array_equal(got, ref) else \
+            f"{int((got != ref).any(axis=1).sum())} blocks differ"
+    return res
+
+
 def _cpu_threads():
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     return max(1, min(threads, os.cpu_count() or 1, 64))
@@ -532,6 +577,10 @@ def main():
         ref_row = bc7.pop("_ref_row", None)
         if args.bc7_shake_ranks > 0:
             bc7_pruned = bc7_secondary(args, gic, src, size, rows, world, dev, rank, args.bc7_shake_ranks, ref_row)
+    enc16 = {}
+    if fmt == 1 and not args.no_bc7enc:
+        enc16["bc7enc16"] = bc7enc16_leg(args, gic, src, size, world, dev, rank, fast=False)
+        enc16["bc7enc16_fast"] = bc7enc16_leg(args, gic, src, size, world, dev, rank, fast=True)
     bc45 = {}
     if fmt == 1 and not args.no_bc45:
         for f in (4, 5):
@@ -583,6 +632,7 @@ def main():
             line["bc7"] = bc7
         if bc7_pruned is not None:
             line["bc7_pruned"] = bc7_pruned
+        line.update(enc16)
         line.update(bc45)
         print(json.dumps(line), flush=True)
     if world > 1:

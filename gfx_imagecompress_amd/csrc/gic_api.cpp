@@ -90,7 +90,7 @@ static int check_options(gic_format fmt, const gic_options &o)
     if (o.adaptive_weights) return GIC_EUNSUP;
     if (o.refinement_steps > 8) return GIC_EINVAL;
     if (fmt == GIC_FMT_BC4 && o.bc4_channel > 3) return GIC_EINVAL;
-    if (fmt == GIC_FMT_BC7 && o.bc7_performance != 1.0f) return GIC_EUNSUP;   // optQuantTrace_d path not built
+    if (o.bc7_performance != o.bc7_performance) return GIC_EINVAL;   // NaN (the reference clamps to [0, 1])
     if (o.bc7_shake_ranks > 8) return GIC_EINVAL;
     if (fmt == GIC_FMT_BC7ENC16 && (o.bc7enc_uber_level > 4 || o.bc7enc_max_partitions > 64)) return GIC_EINVAL;
     return GIC_OK;

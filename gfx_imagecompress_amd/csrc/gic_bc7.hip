@@ -388,6 +388,133 @@ __device__ double opt_quant(const double data[][4], int n, int ncl, int *index, 
 
 #include "bc7_quant.inc"
 
+// ------------------------------------ exhaustive quantiser (performance < 1) ---
+// optQuantTrace_d (amd_bc7_3dquant_vpc.cpp:1425-1554) with quantTrace_d
+// (:1067-1199) walking the traceBuilder tables (:1557-1712), which the host
+// builds once per device (build_trace below).  Step i of table (nc, ne) holds
+// kc = k | code << 5 (k = 2 * entry + 1 if the entry leaves its cluster
+// downwards, the sign of its contribution) and d = 1 / (q2 - q^2 / ne).  The
+// reference's encoder calls it instead of optQuantAnD_d for blocks whose range
+// exceeds 255 * performance, single-index modes with at most 8 clusters
+// (amd_bc7_body.cpp:606-633) and both halves of the dual-index candidates
+// (:1103-1154).  One lane per problem: the walk's double sums run in the
+// reference's order.
+struct TraceTab {
+    const uint32_t *kc;
+    const double *d;
+};
+__constant__ uint32_t dTraceOff[8][16];
+__constant__ uint32_t dTraceCnt[8][16];
+
+__device__ void quant_trace(const double ord[][4], int ne, int nc, int *index, int dim, const TraceTab &tt)
+{
+    const uint32_t off = dTraceOff[nc - 1][ne - 1], cnt = dTraceCnt[nc - 1][ne - 1];
+    double acc[4] = {0., 0., 0., 0.}, best = 0.;
+    int k = -1;
+    for (uint32_t i = 0; i < cnt; ++i) {
+        const uint32_t kc = tt.kc[off + i];
+        const int e = (int)((kc & 31u) >> 1);
+        const bool neg = kc & 1u;
+        double c = 0.;
+        for (int j = 0; j < dim; ++j) {
+            acc[j] += neg ? -ord[e][j] : ord[e][j];
+            c = j ? c + acc[j] * acc[j] : acc[j] * acc[j];
+        }
+        c = c * tt.d[off + i];
+        if (c > best) {
+            best = c;
+            k = (int)i;
+        }
+    }
+    if (k < 0) {
+        for (int i = 0; i < ne; ++i) index[i] = 0;
+        return;
+    }
+    uint32_t bits = tt.kc[off + (uint32_t)k] >> 5;
+    int cl = 0;
+    for (int i = 0; i < ne; ++i) {
+        while (!(bits & 1u)) {
+            ++cl;
+            bits >>= 1;
+        }
+        index[i] = cl;
+        bits >>= 1;
+    }
+}
+
+__device__ double opt_quant_trace(const double data[][4], int n, int ncl, int *index_, int dim, const TraceTab &tt)
+{
+    int index[16], order[16];
+    double cen[16][4], ord[16][4], mean[4], cov[4][4], prj[16], dir[4] = {0, 0, 0, 0};
+    double s, t = 0;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < dim; ++j) cen[i][j] = data[i][j];
+    for (int i = 0; i < dim; ++i) {   // centerInPlace_d
+        mean[i] = 0;
+        for (int k = 0; k < n; ++k) mean[i] += cen[k][i];
+    }
+    if (n)
+        for (int i = 0; i < dim; ++i) {
+            mean[i] /= (double)n;
+            for (int k = 0; k < n; ++k) cen[k][i] -= mean[i];
+        }
+    for (int i = 0; i < dim; ++i)   // covariance_d
+        for (int j = 0; j <= i; ++j) {
+            cov[i][j] = 0;
+            for (int k = 0; k < n; ++k) cov[i][j] += cen[k][i] * cen[k][j];
+        }
+    for (int i = 0; i < dim; ++i)
+        for (int j = i + 1; j < dim; ++j) cov[i][j] = cov[j][i];
+    for (int j = 0; j < dim; ++j) t += cov[j][j];
+    if (t < 0.000001 || n == 0) {   // EPSILON
+        for (int i = 0; i < n; ++i) index_[i] = 0;
+        return 0.;   // every entry at the mean: no error
+    }
+    principal_vector(cov, dir, dim);
+    project(cen, n, dir, prj, dim);
+    for (int it = 0; it < 20; ++it) {   // MAX_TRY
+        if (it) {   // re-project on the least-squares direction; stop once the order holds
+            t = 0;
+            for (int j = 0; j < dim; ++j) {
+                dir[j] = 0;
+                for (int k = 0; k < n; ++k) dir[j] += ord[k][j] * index[k];
+                t += dir[j] * dir[j];
+            }
+            t = sqrt(t) * 0.000001;
+            project(cen, n, dir, prj, dim);
+            int j = 1;
+            while (j < n && !(prj[order[j]] < prj[order[j - 1]] - t)) ++j;
+            if (j >= n) break;
+        }
+        double sd[16];
+        for (int k = 0; k < n; ++k) sd[k] = prj[k], order[k] = k;
+        stable_sort(sd, order, n);   // sortProjection
+        for (int k = 0; k < n; ++k)
+            for (int j = 0; j < dim; ++j) ord[k][j] = cen[order[k]][j];
+        quant_trace(ord, n, ncl, index, dim, tt);
+    }
+    s = t = 0;
+    for (int k = 0; k < n; ++k) {
+        s += index[k];
+        t += index[k] * index[k];
+    }
+    for (int j = 0; j < dim; ++j) {
+        dir[j] = 0;
+        for (int k = 0; k < n; ++k) dir[j] += ord[k][j] * index[k];
+    }
+    s /= (double)n;
+    t = t - s * s * (double)n;
+    t = (t == 0 ? 0. : 1 / t);
+    for (int i = 0; i < n; ++i) index_[order[i]] = index[i];
+    double err = 0;   // totalError_d over the entries in their own order
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < dim; ++j) {
+            const double o = mean[j] + dir[j] * t * (index_[i] - s);
+            err += (data[i][j] - o) * (data[i][j] - o);
+        }
+    return err;
+}
+
 // -------------------------------------------------------------- shakers ---
 
 __device__ void collapse(int *idx, int n)
@@ -1131,6 +1258,8 @@ struct Params {
     // BC7BlockEncoder's quality-derived settings (amd_bc7_body.hpp:94-149),
     // computed on the host exactly as the constructor does
     double quality, shake_thr, err_thr, part_search;
+    double quant_thr;      // m_quantizerRangeThreshold = 255 * performance: above it optQuantTrace_d
+    TraceTab trace;        // its tables (null unless performance < 1)
     uint32_t stage_mask;   // modes evaluated by this launch sequence (all, or one per stage)
     // partitions shaken per mode (CompressSingleIndexBlock's `attempts`,
     // :695-706, optionally capped by gic_options.bc7_shake_ranks), 4 bits per
@@ -1398,6 +1527,45 @@ __global__ void __launch_bounds__(256, 2) k_quant_reg(Params p, Workspace ws, in
 #pragma unroll
         for (int i = 0; i < 16; ++i)
             if ((mask >> i) & 1u) tidx |= (uint64_t)(idx[i] & 15) << (4 * i);
+    }
+    ws.qerr[(size_t)b * kQuantTasks + task] = err;
+    ws.qidx[(size_t)b * kQuantTasks + task] = tidx;
+}
+
+// K1t (performance < 1): optQuantTrace_d for the partitions of the single-index
+// modes with at most 8 clusters (0-3, 7) of blocks whose range exceeds
+// 255 * performance (CompressSingleIndexBlock :606-633); overwrites what the
+// optQuantAnD_d kernels stored for them.  Lanes of a wave share a task, so
+// they walk the same trace table.
+__global__ void __launch_bounds__(64) k_quant_trace(Params p, Workspace ws)
+{
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t t = gid / p.n, b = gid % p.n;
+    if (t >= 272u) return;
+    const int task = (int)(t < 208u ? t : t + 1u);   // skip mode 6 (16 clusters: optQuantAnD_d)
+    int mode, part;
+    task_mode(task, mode, part);
+    const BlockMeta meta = ws.meta[b];
+    if (!mode_active(meta, p, mode) || !(meta.max_range > p.quant_thr)) return;
+    if (part >= mode_tries(p, mode)) return;
+    const ModeInfo &mi = kModes[mode];
+    const int dim = mi.enc == ENC_NO_ALPHA ? 3 : 4;
+    const int ncl = 1 << mi.ib0;
+    const float *tex = ws.tex + (size_t)b * 64;
+    double err = 0.;
+    uint64_t tidx = 0;
+    for (int sub = 0; sub < mi.subsets; ++sub) {
+        double d[16][4];
+        int tex_of[16], n = 0;
+        for (int i = 0; i < 16; ++i)
+            if ((int)shape_of(mi.subsets, part, i) == sub) {
+                for (int j = 0; j < dim; ++j) d[n][j] = (double)tex[i * 4 + j];
+                tex_of[n++] = i;
+            }
+        if (!n) continue;
+        int idx[16];
+        err += opt_quant_trace(d, n, ncl, idx, dim, p.trace);
+        for (int k = 0; k < n; ++k) tidx |= (uint64_t)(idx[k] & 15) << (4 * tex_of[k]);
     }
     ws.qerr[(size_t)b * kQuantTasks + task] = err;
     ws.qidx[(size_t)b * kQuantTasks + task] = tidx;
@@ -1795,6 +1963,35 @@ __global__ void __launch_bounds__(256) k_dual_quant(Params p, Workspace ws)
     ws.dqerr[((size_t)b * kDualTasks + task) * 2 + half] = qe;
 }
 
+// K3t (performance < 1): optQuantTrace_d for both halves of the dual-index
+// candidates of blocks whose range exceeds 255 * performance
+// (CompressDualIndexBlock :1103-1154); overwrites the optQuantAnD_d results.
+__global__ void __launch_bounds__(64) k_dual_quant_trace(Params p, Workspace ws)
+{
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t r = gid / p.n, b = gid % p.n;
+    if (r >= kDualTasks * 2) return;
+    const uint32_t task = r >> 1, half = r & 1;
+    int mode, rot, sel;
+    dual_task(task, mode, rot, sel);
+    const BlockMeta meta = ws.meta[b];
+    if (!mode_active(meta, p, mode) || !(meta.max_range > p.quant_thr)) return;
+    const ModeInfo &mi = kModes[mode];
+    const float *tex = ws.tex + (size_t)b * 64;
+    const int ncl = 1 << dual_index_bits(mi, (int)half, sel);
+    double blk[16][4];
+    for (int i = 0; i < 16; ++i) {
+        for (int j = 0; j < 3; ++j) blk[i][j] = (double)tex[i * 4 + kRot[rot][half ? 0 : j + 1]];
+        blk[i][3] = 0.0;
+    }
+    int idx[16];
+    const double qe = opt_quant_trace(blk, 16, ncl, idx, 3, p.trace);
+    uint64_t ti = 0;
+    for (int k = 0; k < 16; ++k) ti |= (uint64_t)(idx[k] & 15) << (4 * k);
+    ws.dqidx[((size_t)b * kDualTasks + task) * 2 + half] = ti;
+    ws.dqerr[((size_t)b * kDualTasks + task) * 2 + half] = qe;
+}
+
 // K3b (waves): shakers of one half of a dual-index candidate
 // (CompressDualIndexBlock :1158-1254); integral blocks
 __global__ void __launch_bounds__(256, 4) k_dual_wave(Params p, Workspace ws, const SpEntry *__restrict__ sp)
@@ -2115,6 +2312,82 @@ static int build_subset_problems(std::vector<uint32_t> &prob, std::vector<uint32
 }
 static int g_nu = 0;
 
+// traceBuilder (amd_bc7_3dquant_vpc.cpp:1557-1712) for ne entries and nc
+// clusters, appended to kc/d.  Seven nested loops (one per delimiter, each
+// running its positions in the direction given by the parity of its start:
+// the reference's DIG macro; a level past nc - 2 runs once) drive a body
+// that moves every delimiter one step towards its target position, keeping
+// per-cluster counts h (a move that would empty a cluster below zero or put
+// every entry in one cluster is retried after the others), and records each
+// move.  A jump of more than one position ends the build with no steps, as
+// the reference's early return leaves its count at zero.
+struct TraceBuild {
+    int ne, nc, n, j[7], k[7], h[8], q, q2, cd;
+    std::vector<uint32_t> *kc;
+    std::vector<double> *d;
+    size_t start;
+};
+
+static bool trace_body(TraceBuild &b)
+{
+    bool rescan;
+    long guard = 0;
+    do {
+        rescan = false;
+        for (int p = 0; p < b.nc - 1; ++p) {
+            const int dj = b.j[p] - b.k[p];
+            if (dj < -1 || dj > 1) return false;
+            if (!dj) continue;
+            const int entry = dj > 0 ? b.k[p] - p : b.j[p] - p;
+            const int from = dj > 0 ? p + 1 : p, to = dj > 0 ? p : p + 1;
+            if (b.h[from] - 1 < 0 || b.h[to] + 1 >= b.ne) {
+                rescan = true;
+                continue;
+            }
+            --b.h[from];
+            ++b.h[to];
+            b.q2 += dj > 0 ? 1 - 2 * from : 2 * from + 1;
+            b.q += dj > 0 ? -1 : 1;
+            b.cd = (b.cd | (1 << b.k[p])) & ~(1 << b.j[p]);
+            b.kc->push_back((uint32_t)(dj > 0 ? 2 * entry + 1 : 2 * entry) | ((uint32_t)b.cd & 0x7FFFFFFu) << 5);
+            b.d->push_back(1. / ((double)b.q2 - (double)b.q * (double)b.q / (double)b.ne));
+            b.k[p] = b.j[p];
+        }
+    } while (rescan && ++guard < 1000000);
+    return true;
+}
+
+static bool trace_levels(TraceBuild &b, int p, int jin)
+{
+    const bool used = b.nc >= p + 2;
+    for (int i = jin; i < b.n || !used; ++i) {
+        b.j[p] = ((jin & 1) == (p & 1)) ? i : b.n - 1 - (i - jin);
+        if (!(p < 6 ? trace_levels(b, p + 1, b.j[p] + 1) : trace_body(b))) return false;
+        if (!used) break;
+    }
+    return true;
+}
+
+static uint32_t build_trace(int ne, int nc, std::vector<uint32_t> &kc, std::vector<double> &d)
+{
+    if (nc == 1) return 0;
+    TraceBuild b{};
+    b.ne = ne, b.nc = nc, b.n = ne + nc - 2;
+    for (int p = 0; p < 7; ++p) b.k[p] = p;
+    b.h[nc - 1] = ne;
+    b.q = ne * (nc - 1);
+    b.q2 = ne * (nc - 1) * (nc - 1);
+    b.cd = -(1 << (nc - 1));
+    b.kc = &kc, b.d = &d;
+    const size_t start = kc.size();
+    if (!trace_levels(b, 0, 0)) {
+        kc.resize(start);
+        d.resize(start);
+        return 0;
+    }
+    return (uint32_t)(kc.size() - start);
+}
+
 // Per-device state: the single-point table, and two chunk workspaces with two
 // internal streams, so that consecutive chunks run concurrently (one chunk's
 // quantiser beside the other's shakers, and each launch's tail beside the
@@ -2128,7 +2401,38 @@ struct DeviceState {
     Workspace ws[2]{};
     hipStream_t lane[2] = {nullptr, nullptr};
     hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
+    TraceTab trace{nullptr, nullptr};   // optQuantTrace_d tables, built on first use (performance < 1)
 };
+
+// Caller holds g_state_lock.
+static hipError_t get_trace(DeviceState &st)
+{
+    if (st.trace.kc) return hipSuccess;
+    std::vector<uint32_t> kc;
+    std::vector<double> d;
+    uint32_t off[8][16], cnt[8][16];
+    for (int nc = 1; nc <= 8; ++nc)
+        for (int ne = 1; ne <= 16; ++ne) {
+            off[nc - 1][ne - 1] = (uint32_t)kc.size();
+            cnt[nc - 1][ne - 1] = build_trace(ne, nc, kc, d);
+        }
+    uint32_t *dkc = nullptr;
+    double *dd = nullptr;
+    hipError_t e = hipMalloc(&dkc, kc.size() * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&dd, d.size() * sizeof(double));
+    if (e == hipSuccess) e = hipMemcpy(dkc, kc.data(), kc.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dd, d.data(), d.size() * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dTraceOff), off, sizeof(off));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dTraceCnt), cnt, sizeof(cnt));
+    if (e != hipSuccess) {
+        (void)hipFree(dkc);
+        (void)hipFree(dd);
+        return e;
+    }
+    st.trace.kc = dkc;
+    st.trace.d = dd;
+    return hipSuccess;
+}
 
 static std::mutex g_state_lock;
 static DeviceState g_states[64];
@@ -2249,6 +2553,10 @@ static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, h
         }
         if (sm & 0xC0u)
             hipLaunchKernelGGL(k_quant_reg<4>, dim3((uint32_t)((nq4 + wg - 1) / wg)), dim3(wg), 0, s, p, ws, 208, 65);
+        if (p.quant_thr < 255.0 && (sm & 0x8Fu)) {
+            const uint64_t nt = (uint64_t)p.n * 272;
+            hipLaunchKernelGGL(k_quant_trace, dim3((uint32_t)((nt + 63) / 64)), dim3(64), 0, s, p, ws);
+        }
         const uint64_t ns = (uint64_t)p.n * kShakeSlots * kShakeRanks;
         hipLaunchKernelGGL(k_shake, dim3((uint32_t)((ns + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
         if ((sm & 0x03u) && wave_count<8>(p.att)) {
@@ -2268,6 +2576,8 @@ static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, h
         const uint64_t ndq = (uint64_t)p.n * kDualTasks * 2;
         hipLaunchKernelGGL(k_dual_quant, dim3((uint32_t)((ndq + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
         hipLaunchKernelGGL(k_dual_quant_reg, dim3((uint32_t)((ndq + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
+        if (p.quant_thr < 255.0)
+            hipLaunchKernelGGL(k_dual_quant_trace, dim3((uint32_t)((ndq + 63) / 64)), dim3(64), 0, s, p, ws);
         const uint64_t nd = (uint64_t)p.n * kDualTasks;
         hipLaunchKernelGGL(k_dual, dim3((uint32_t)((nd + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
         const uint64_t ndw = (uint64_t)p.n * kDualTasks * 2 * 64;
@@ -2296,6 +2606,13 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
     DeviceState *st = nullptr;
     hipError_t e = get_state(chunk, nsets, st);
     if (e != hipSuccess) return e;
+    // BC7BlockEncoder ctor: m_performance clamped to [0, 1], m_quantizerRangeThreshold
+    // = 255 * m_performance (amd_bc7_body.hpp:109-116)
+    const double perf = o.bc7_performance < 1.0 ? (o.bc7_performance > 0.0 ? (double)o.bc7_performance : 0.0) : 1.0;
+    if (perf < 1.0) {
+        e = get_trace(*st);
+        if (e != hipSuccess) return e;
+    }
     e = hipEventRecord(st->ev_fork, s);   // fork: the lanes start after the caller's prior work
     for (int k = 0; k < nsets && e == hipSuccess; ++k) e = hipStreamWaitEvent(st->lane[k], st->ev_fork, 0);
     if (e != hipSuccess) return e;
@@ -2327,6 +2644,8 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
             p.err_thr = 0;
             p.part_search = 1.0;
         }
+        p.quant_thr = 255 * perf;
+        p.trace = st->trace;
         p.att = host_attempts(p, o.bc7_shake_ranks);
         p.decode_select = o.bc7_shake_ranks > 0 && !(p.err_thr > 0);
         p.dual_cap = 2 * (int)o.bc7_shake_ranks;

@@ -60,7 +60,8 @@ typedef struct gic_options {
     uint8_t alpha_restrict;      /* default 1 */
     uint8_t force_alpha_one;     /* 1: ignore source alpha (ReadNxNBlockF forceAlphaTo1) */
     float bc7_quality;           /* BC7BlockEncoder quality, clamped to [0,1] (default 1.0) */
-    float bc7_performance;       /* must be 1.0 in this release */
+    float bc7_performance;       /* BC7BlockEncoder performance, clamped to [0,1] (default 1.0); blocks whose
+                                    range exceeds 255 * performance use the exhaustive optQuantTrace_d quantiser */
     uint32_t bc7_shake_ranks;    /* partitions shaken per single-index BC7 mode: 0 = the reference's
                                     count (8 at quality 1, bit-exact search); 1..8 caps it (pruned
                                     search, held to the per-block MSE tolerance) */

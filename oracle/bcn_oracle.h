@@ -81,6 +81,15 @@ int orc_encode_image_bc7_ex(const uint8_t *src, uint32_t width, uint32_t height,
 void orc_bc7enc_block(const uint8_t rgba[64], int fast, int perceptual, uint8_t out[16]);
 int orc_encode_image_bc7enc(const uint8_t *src, uint32_t width, uint32_t height, uint32_t slices, uint32_t channels,
                             int fast, int perceptual, uint8_t *dst);
+/* the same through the image driver's block-row range and thread pool */
+int orc_encode_image_bc7enc_rows(const uint8_t *src, uint32_t width, uint32_t height, uint32_t slices,
+                                 uint32_t channels, int32_t first_row, int32_t num_rows, int threads, int fast,
+                                 int perceptual, uint8_t *dst);
+
+/* the BC7 block loop with the encoder's performance as well (optQuantTrace_d below 1) */
+int orc_encode_image_bc7_perf(const uint8_t *src, uint32_t width, uint32_t height, uint32_t slices, uint32_t channels,
+                              int32_t first_row, int32_t num_rows, int threads, float quality, uint8_t mode_mask,
+                              float performance, uint8_t *dst, double *block_err);
 
 /* helpers exposed for unit tests */
 void orc_load_block_rgba8(const uint8_t *src, uint32_t width, uint32_t height,
@@ -91,6 +100,10 @@ uint64_t orc_fnv1a64(const uint8_t *p, size_t n);
 int orc_bc7_shake_ramp(int clog, int bits, int p1, int p2, int i);
 /* optQuantAnD_d on caller data, data4 = n x 4 doubles (test hook) */
 double orc_bc7_opt_quant(const double *data4, int n, int ncl, int *index, int dim);
+/* optQuantTrace_d on caller data (n <= 16), and the traceBuilder tables (test hooks) */
+double orc_bc7_opt_quant_trace(const double *data4, int n, int ncl, int *index, int dim);
+int orc_bc7_trace_len(int nc, int ne);
+void orc_bc7_trace_step(int nc, int ne, int i, int *k, int *code, double *d);
 /* decode one BC7 block to RGBA8 (for tolerance checks) */
 void orc_bc7_decode(const uint8_t blk[16], uint8_t rgba[64]);
 void orc_bc7_decode_n(const uint8_t *blk, size_t n, uint8_t *rgba);

@@ -10,8 +10,10 @@
  * reference's association order (build with -ffp-contract=off).  Sorts whose
  * ties matter use a stable sort, matching glibc 2.35's merge-sort qsort.
  *
- * Not restated (outside the default path; rejected with a negative error):
- * optQuantTrace_d (only reached when performance < 1, amd_bc7_body.cpp:606).
+ * optQuantTrace_d + quantTrace_d + traceBuilder (amd_bc7_3dquant_vpc.cpp:
+ * 1067-1199, 1425-1712) are restated too: the exhaustive quantiser the
+ * encoder uses instead of optQuantAnD_d when performance < 1 and the block's
+ * range exceeds 255 * performance (amd_bc7_body.cpp:606-633, :1103-1154).
  *
  * Shaker ramps: amd_shake.cpp:236 tests USE_FINAL_BC7_WEIGHTS, which is only
  * defined in amd_bc7_body.cpp:60, so that translation unit builds its ramp
@@ -22,6 +24,7 @@
 #include <float.h>
 #include <math.h>
 #include <pthread.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "bc7_tables.h"
@@ -408,6 +411,249 @@ double orc_bc7_opt_quant(const double *data4, int n, int ncl, int *index, int di
     for (int i = 0; i < n; ++i)
         for (int j = 0; j < 4; ++j) d[i][j] = data4[i * 4 + j];
     return opt_quant(d, n, ncl, index, o, dim);
+}
+
+
+/* --------------------------- exhaustive trace quantiser (performance < 1) --- */
+/* traceBuilder, amd_bc7_3dquant_vpc.cpp:1557-1712: for ne sorted entries and nc
+ * clusters, a walk over every monotone assignment of entries to clusters in
+ * which each step moves one cluster delimiter by one position (delimiter p
+ * visits its positions in alternating direction, the nested DIG loops).  A
+ * step records the moved entry with its sign (k = 2 ci [+1]), the reciprocal
+ * of the index variance q2 - q^2/ne after it (d) and the occupancy bit code of
+ * the positions (1 = entry, 0 = delimiter).  The reference stops building when
+ * a delimiter would jump by more than one position, leaving the step count at
+ * its zero initialisation; this restatement does the same. */
+#define TRACE_CAP 250000   /* MAX_TRACE */
+typedef struct {
+    int ne, nc, n;
+    int j[7], k[7], h[8];
+    int q, q2, cd, c;
+    int *tk, *code;
+    double *td;
+} trace_build;
+
+/* the innermost body of traceBuilder: returns 1 when the reference returns */
+static int trace_body(trace_build *b)
+{
+    int rescan, guard = 0;
+    do {
+        rescan = 0;
+        for (int p = 0; p < b->nc - 1; ++p) {
+            const int dj = b->j[p] - b->k[p];
+            if (dj > 1 || dj < -1) return 1;
+            if (dj == 0) continue;
+            /* dj = 1: the entry above delimiter p drops to cluster p; -1: rises */
+            const int ci = dj == 1 ? b->k[p] - p : b->j[p] - p;
+            const int from = dj == 1 ? p + 1 : p, to = dj == 1 ? p : p + 1;
+            b->h[from]--;
+            b->h[to]++;
+            if (b->h[from] < 0 || b->h[to] >= b->ne) {
+                b->h[from]++;
+                b->h[to]--;
+                rescan = 1;
+                continue;
+            }
+            if (dj == 1) {
+                b->q2 += -2 * from + 1;
+                b->q--;
+            } else {
+                b->q2 += 2 * from + 1;
+                b->q++;
+            }
+            b->cd |= 1 << b->k[p];
+            b->cd &= ~(1 << b->j[p]);
+            if (b->c >= TRACE_CAP) return 1;   /* never reached for ne <= 16, nc <= 8 */
+            b->tk[b->c] = dj == 1 ? 2 * ci + 1 : 2 * ci;
+            b->td[b->c] = 1. / ((double)b->q2 - (double)b->q * (double)b->q / (double)b->ne);
+            b->code[b->c] = b->cd;
+            b->c++;
+            b->k[p] = b->j[p];
+        }
+    } while (rescan && ++guard < 1000000);
+    return 0;
+}
+
+/* level p of the DIG nest: delimiter p over [jin, n), direction by parity */
+static int trace_level(trace_build *b, int p, int jin)
+{
+    for (int i = jin; i < b->n || b->nc < p + 2; ++i) {
+        b->j[p] = ((jin & 1) == (p & 1)) ? i : b->n - 1 - (i - jin);
+        const int stop = p < 6 ? trace_level(b, p + 1, b->j[p] + 1) : trace_body(b);
+        if (stop) return 1;
+        if (b->nc < p + 2) break;
+    }
+    return 0;
+}
+
+static int *g_trk[8][16], *g_trcode[8][16];
+static double *g_trd[8][16];
+static int g_trcnt[8][16];
+static pthread_once_t g_trace_once = PTHREAD_ONCE_INIT;
+
+static void build_traces(void)
+{
+    static int tk[TRACE_CAP], code[TRACE_CAP];
+    static double td[TRACE_CAP];
+    for (int nc = 1; nc <= 8; ++nc)
+        for (int ne = 1; ne <= 16; ++ne) {
+            int cnt = 0;
+            if (nc > 1) {
+                trace_build b;
+                memset(&b, 0, sizeof(b));
+                b.ne = ne, b.nc = nc, b.n = ne + nc - 2;
+                for (int p = 0; p < 7; ++p) b.k[p] = p;
+                b.h[nc - 1] = ne;
+                b.q = ne * (nc - 1);
+                b.q2 = ne * (nc - 1) * (nc - 1);
+                b.cd = -(1 << (nc - 1));
+                b.tk = tk, b.td = td, b.code = code;
+                cnt = trace_level(&b, 0, 0) ? 0 : b.c;
+            }
+            g_trcnt[nc - 1][ne - 1] = cnt;
+            g_trk[nc - 1][ne - 1] = (int *)malloc(sizeof(int) * (size_t)(cnt + 1));
+            g_trcode[nc - 1][ne - 1] = (int *)malloc(sizeof(int) * (size_t)(cnt + 1));
+            g_trd[nc - 1][ne - 1] = (double *)malloc(sizeof(double) * (size_t)(cnt + 1));
+            memcpy(g_trk[nc - 1][ne - 1], tk, sizeof(int) * (size_t)cnt);
+            memcpy(g_trcode[nc - 1][ne - 1], code, sizeof(int) * (size_t)cnt);
+            memcpy(g_trd[nc - 1][ne - 1], td, sizeof(double) * (size_t)cnt);
+        }
+}
+
+/* test hook: a trace table's length, and step i's (k, code, d) */
+int orc_bc7_trace_len(int nc, int ne)
+{
+    pthread_once(&g_trace_once, build_traces);
+    return g_trcnt[nc - 1][ne - 1];
+}
+void orc_bc7_trace_step(int nc, int ne, int i, int *k, int *code, double *d)
+{
+    pthread_once(&g_trace_once, build_traces);
+    *k = g_trk[nc - 1][ne - 1][i];
+    *code = g_trcode[nc - 1][ne - 1][i];
+    *d = g_trd[nc - 1][ne - 1][i];
+}
+
+/* quantTrace_d, amd_bc7_3dquant_vpc.cpp:1067-1199: walk the trace keeping the
+ * first step of largest |sum of signed entries|^2 * d, decode its code. */
+static void quant_trace(double data[][4], int ne, int nc, int *index, int dim)
+{
+    const int cnt = g_trcnt[nc - 1][ne - 1];
+    const int *tk = g_trk[nc - 1][ne - 1], *code = g_trcode[nc - 1][ne - 1];
+    const double *td = g_trd[nc - 1][ne - 1];
+    double acc[4] = {0, 0, 0, 0}, best = 0;
+    int k = -1;
+    for (int i = 0; i < cnt; ++i) {
+        const int e = tk[i] >> 1;
+        const double sg = (tk[i] & 1) ? -1.0 : 1.0;
+        double c = 0;
+        for (int j = 0; j < dim; ++j) {
+            acc[j] += sg * data[e][j];   /* sdata[2e+1] = -data[e]: negation is exact */
+            c = j ? c + acc[j] * acc[j] : acc[j] * acc[j];
+        }
+        c = c * td[i];
+        if (c > best) {
+            k = i;
+            best = c;
+        }
+    }
+    if (k < 0) {
+        for (int i = 0; i < ne; ++i) index[i] = 0;
+        return;
+    }
+    int bits = code[k], cl = 0;
+    for (int i = 0; i < ne; ++i) {
+        while (!(bits & 1)) {
+            cl++;
+            bits >>= 1;
+        }
+        index[i] = cl;
+        bits >>= 1;
+    }
+}
+
+/* optQuantTrace_d, amd_bc7_3dquant_vpc.cpp:1425-1554 */
+static double opt_quant_trace(double data[][4], int n, int ncl, int *index_, double out[][4], int dim)
+{
+    pthread_once(&g_trace_once, build_traces);
+    int index[16], order[16];
+    double cen[16][4], ord[16][4], mean[4], cov[4][4], prj[16], dir[4] = {0, 0, 0, 0};
+    double s, t = 0;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < dim; ++j) cen[i][j] = data[i][j];
+    for (int i = 0; i < dim; ++i) {   /* centerInPlace_d */
+        mean[i] = 0;
+        for (int k = 0; k < n; ++k) mean[i] += cen[k][i];
+    }
+    if (n)
+        for (int i = 0; i < dim; ++i) {
+            mean[i] /= (double)n;
+            for (int k = 0; k < n; ++k) cen[k][i] -= mean[i];
+        }
+    for (int i = 0; i < dim; ++i)   /* covariance_d */
+        for (int j = 0; j <= i; ++j) {
+            cov[i][j] = 0;
+            for (int k = 0; k < n; ++k) cov[i][j] += cen[k][i] * cen[k][j];
+        }
+    for (int i = 0; i < dim; ++i)
+        for (int j = i + 1; j < dim; ++j) cov[i][j] = cov[j][i];
+    for (int j = 0; j < dim; ++j) t += cov[j][j];
+    if (t < 0.000001 || n == 0) {   /* EPSILON */
+        for (int i = 0; i < n; ++i) {
+            index_[i] = 0;
+            for (int j = 0; j < dim; ++j) out[i][j] = mean[j];
+        }
+        return 0.;
+    }
+    principal_vector(cov, dir, dim);
+    project(cen, n, dir, prj, dim);
+    for (int it = 0; it < 20; ++it) {   /* MAX_TRY */
+        if (it) {
+            t = 0;
+            for (int j = 0; j < dim; ++j) {
+                dir[j] = 0;
+                for (int k = 0; k < n; ++k) dir[j] += ord[k][j] * index[k];
+                t += dir[j] * dir[j];
+            }
+            t = sqrt(t) * 0.000001;
+            project(cen, n, dir, prj, dim);
+            int j = 1;
+            while (j < n && !(prj[order[j]] < prj[order[j - 1]] - t)) ++j;
+            if (j >= n) break;   /* the order is stable: done */
+        }
+        sort_order(prj, order, n);
+        for (int k = 0; k < n; ++k)
+            for (int j = 0; j < dim; ++j) ord[k][j] = cen[order[k]][j];
+        quant_trace(ord, n, ncl, index, dim);
+    }
+    double q = 0;
+    s = t = 0;
+    for (int k = 0; k < n; ++k) {
+        s += index[k];
+        t += index[k] * index[k];
+    }
+    for (int j = 0; j < dim; ++j) {
+        dir[j] = 0;
+        for (int k = 0; k < n; ++k) dir[j] += ord[k][j] * index[k];
+        q += dir[j] * dir[j];
+    }
+    s /= (double)n;
+    t = t - s * s * (double)n;
+    t = (t == 0 ? 0. : 1 / t);
+    for (int i = 0; i < n; ++i) {
+        for (int j = 0; j < dim; ++j) out[order[i]][j] = mean[j] + dir[j] * t * (index[i] - s);
+        index_[order[i]] = index[i];
+    }
+    return total_error(data, out, n, dim);
+}
+
+/* test hook: optQuantTrace_d on caller data (n <= 16) */
+double orc_bc7_opt_quant_trace(const double *data4, int n, int ncl, int *index, int dim)
+{
+    double d[16][4], o[16][4];
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < 4; ++j) d[i][j] = data4[i * 4 + j];
+    return opt_quant_trace(d, n, ncl, index, o, dim);
 }
 
 /* -------------------------------------------------------- shakers --- */
@@ -1071,12 +1317,10 @@ static double single_index(bc7_enc *e, double in[16][4], uint8_t out[16], int mo
             if (!cnt[s]) continue;
             int idx[16];
             double o[16][4];
-            if (e->clusters[0] > 8 || e->max_range <= e->quant_thr) {
+            if (e->clusters[0] > 8 || e->max_range <= e->quant_thr)
                 err += opt_quant(sub[s], cnt[s], e->clusters[0], idx, o, dim);
-            } else {
-                e->unsupported = 1;
-                return DBL_MAX;
-            }
+            else
+                err += opt_quant_trace(sub[s], cnt[s], e->clusters[0], idx, o, dim);
             for (int k = 0; k < cnt[s]; ++k) e->stored[part][s][k] = idx[k];
         }
         e->stored_err[part] = err;
@@ -1269,12 +1513,13 @@ static double dual_index(bc7_enc *e, double in[16][4], uint8_t out[16], int mode
         }
         for (int sel = 0; sel < nsel; ++sel) {
             double qe = 0.;
-            if (!(e->max_range <= e->quant_thr)) {
-                e->unsupported = 1;
-                return DBL_MAX;
+            if (e->max_range <= e->quant_thr) {
+                qe = opt_quant(cb, 16, 1 << ibs[sel], idx[0], oq[0], 3);
+                qe += opt_quant(ab, 16, 1 << ibs[1 ^ sel], idx[1], oq[1], 3) / 3.;
+            } else {   /* optQuantTrace_d (:1116-1154) */
+                qe = opt_quant_trace(cb, 16, 1 << ibs[sel], idx[0], oq[0], 3);
+                qe += opt_quant_trace(ab, 16, 1 << ibs[1 ^ sel], idx[1], oq[1], 3) / 3.;
             }
-            qe = opt_quant(cb, 16, 1 << ibs[sel], idx[0], oq[0], 3);
-            qe += opt_quant(ab, 16, 1 << ibs[1 ^ sel], idx[1], oq[1], 3) / 3.;
             if (e->rank_cap > 0 ? qrank[rot * nsel + sel] < 2 * e->rank_cap : (e->quality > 0.7 || qe <= best_q)) {
                 unsigned shake = (unsigned)(6 * e->quality);
                 shake = shake < 6 ? shake : 6;

@@ -59,12 +59,16 @@ typedef struct {
     float bc7_quality;   /* BC7BlockEncoder quality (image API: 1.0) */
     uint8_t bc7_mask;    /* BC7 ModeMask (image API default 0xFF) */
     int bc7_ranks;       /* shake-rank cap (0 = reference) */
+    int enc_fast, enc_perceptual;   /* bc7enc16 (fmt 8) settings */
+    float bc7_perf;      /* BC7BlockEncoder performance (image API: 1.0) */
     int next;            /* next job (slice*nrows + row) */
     int njobs;
     pthread_mutex_t lock;
 } job_t;
 
 static size_t block_bytes(int fmt) { return (fmt == 1 || fmt == 4) ? 8 : 16; }
+static int g_enc_fast, g_enc_perceptual;   /* set by orc_encode_image_bc7enc_rows before the pool runs */
+static __thread float t_bc7_perf = 1.0f;   /* set by orc_encode_image_bc7_perf for its own call */
 
 static void encode_row(job_t *j, uint32_t slice, uint32_t brow)
 {
@@ -106,8 +110,19 @@ static void encode_row(job_t *j, uint32_t slice, uint32_t brow)
             break;
         case 7:
             /* Image_CompressAMDBC7 (amd_bc7_compressor.cpp:58-65) */
-            e = orc_bc7_block_ex(blk, j->bc7_mask, has_alpha, j->bc7_quality, 1, 1, 1.0f, j->bc7_ranks, o);
+            e = orc_bc7_block_ex(blk, j->bc7_mask, has_alpha, j->bc7_quality, 1, 1, j->bc7_perf, j->bc7_ranks, o);
             break;
+        case 8: {
+            /* Image_CompressRichGel999BC7 (richgel999_bc7enc16.cpp:50-57): the float
+             * block back to RGBA8 -- the identity on v / 255.0f */
+            uint8_t px[64];
+            for (int i = 0; i < 64; ++i) {
+                const float v = blk[i] < 0.f ? 0.f : (blk[i] > 1.f ? 1.f : blk[i]);
+                px[i] = (uint8_t)(v * 255.0f + 0.5f);
+            }
+            orc_bc7enc_block(px, j->enc_fast, j->enc_perceptual, o);
+            break;
+        }
         }
         if (j->err) j->err[out_row + bx] = e;
     }
@@ -131,7 +146,7 @@ static int encode_image(int fmt, const uint8_t *src, uint32_t width, uint32_t he
                         float bc7_quality, uint8_t bc7_mask, int bc7_ranks, uint8_t *dst, double *block_err)
 {
     if (!src || !dst || !width || !height || !slices || channels < 1 || channels > 4) return -1;
-    if (fmt < 1 || fmt > 7 || fmt == 6) return -1;
+    if (fmt < 1 || fmt > 8 || fmt == 6) return -1;
     job_t j;
     memset(&j, 0, sizeof(j));
     j.fmt = fmt;
@@ -144,6 +159,9 @@ static int encode_image(int fmt, const uint8_t *src, uint32_t width, uint32_t he
     j.bc7_quality = bc7_quality;
     j.bc7_mask = bc7_mask;
     j.bc7_ranks = bc7_ranks;
+    j.enc_fast = g_enc_fast;
+    j.bc7_perf = t_bc7_perf;
+    j.enc_perceptual = g_enc_perceptual;
     j.bx_count = (width + 3) / 4;
     j.by_count = (height + 3) / 4;
     j.row0 = first_row < 0 ? 0 : (uint32_t)first_row;
@@ -187,4 +205,25 @@ int orc_encode_image_bc7_ex(const uint8_t *src, uint32_t width, uint32_t height,
 {
     return encode_image(7, src, width, height, slices, channels, 0, first_row, num_rows, threads, quality,
                         mode_mask, shake_ranks, dst, block_err);
+}
+
+int orc_encode_image_bc7enc_rows(const uint8_t *src, uint32_t width, uint32_t height, uint32_t slices,
+                                 uint32_t channels, int32_t first_row, int32_t num_rows, int threads, int fast,
+                                 int perceptual, uint8_t *dst)
+{
+    g_enc_fast = fast;
+    g_enc_perceptual = perceptual;
+    return encode_image(8, src, width, height, slices, channels, 0, first_row, num_rows, threads, 1.0f, 0xFF, 0,
+                        dst, NULL);
+}
+
+int orc_encode_image_bc7_perf(const uint8_t *src, uint32_t width, uint32_t height, uint32_t slices, uint32_t channels,
+                              int32_t first_row, int32_t num_rows, int threads, float quality, uint8_t mode_mask,
+                              float performance, uint8_t *dst, double *block_err)
+{
+    t_bc7_perf = performance;
+    const int rc = encode_image(7, src, width, height, slices, channels, 0, first_row, num_rows, threads, quality,
+                                mode_mask, 0, dst, block_err);
+    t_bc7_perf = 1.0f;
+    return rc;
 }

@@ -41,6 +41,16 @@ def lib() -> ctypes.CDLL:
                                                  ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int,
                                                  ctypes.c_float, ctypes.c_uint8, ctypes.c_int, vp, vp]
         _lib.orc_encode_image_bc7_ex.restype = ctypes.c_int
+        _lib.orc_encode_image_bc7_perf.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                   ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int,
+                                                   ctypes.c_float, ctypes.c_uint8, ctypes.c_float, vp, vp]
+        _lib.orc_encode_image_bc7_perf.restype = ctypes.c_int
+        _lib.orc_bc7_opt_quant_trace.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int]
+        _lib.orc_bc7_opt_quant_trace.restype = ctypes.c_double
+        _lib.orc_bc7_opt_quant.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int]
+        _lib.orc_bc7_opt_quant.restype = ctypes.c_double
+        _lib.orc_bc7_trace_len.argtypes = [ctypes.c_int, ctypes.c_int]
+        _lib.orc_bc7_trace_len.restype = ctypes.c_int
         _lib.orc_bc1_block.argtypes = [vp, ctypes.c_int, ctypes.c_float, vp]
         _lib.orc_bc4_block.argtypes = [vp, vp]
         _lib.orc_rgb4_block.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
@@ -59,6 +69,10 @@ def lib() -> ctypes.CDLL:
         _lib.orc_encode_image_bc7enc.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                                  ctypes.c_uint32, ctypes.c_int, ctypes.c_int, vp]
         _lib.orc_encode_image_bc7enc.restype = ctypes.c_int
+        _lib.orc_encode_image_bc7enc_rows.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                      ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int,
+                                                      ctypes.c_int, ctypes.c_int, vp]
+        _lib.orc_encode_image_bc7enc_rows.restype = ctypes.c_int
     return _lib
 
 
@@ -88,7 +102,8 @@ def encode_image(fmt: int, img: np.ndarray, bc4_channel: int = 1, first_row: int
 
 
 def encode_image_bc7(img: np.ndarray, quality: float = 1.0, mode_mask: int = 0xFF, first_row: int = -1,
-                     num_rows: int = -1, threads: int = 0, want_err: bool = False, shake_ranks: int = 0):
+                     num_rows: int = -1, threads: int = 0, want_err: bool = False, shake_ranks: int = 0,
+                     performance: float = 1.0):
     """BC7 over an image with the encoder quality / ModeMask of the block API;
     shake_ranks > 0 models the GPU's pruned search (gic_options.bc7_shake_ranks)."""
     a = np.ascontiguousarray(img, dtype=np.uint8)
@@ -102,8 +117,16 @@ def encode_image_bc7(img: np.ndarray, quality: float = 1.0, mode_mask: int = 0xF
     out = np.zeros((s * rows * bx, 16), np.uint8)
     err = np.zeros(s * rows * bx, np.float64) if want_err else None
     threads = threads or min(os.cpu_count() or 1, 16)
-    rc = lib().orc_encode_image_bc7_ex(a.ctypes.data, w, h, s, c, first_row, num_rows, threads, quality, mode_mask,
-                                       shake_ranks, out.ctypes.data, err.ctypes.data if want_err else None)
+    if performance != 1.0:
+        if shake_ranks:
+            raise ValueError("the oracle models performance < 1 with the reference search only")
+        rc = lib().orc_encode_image_bc7_perf(a.ctypes.data, w, h, s, c, first_row, num_rows, threads, quality,
+                                             mode_mask, performance, out.ctypes.data,
+                                             err.ctypes.data if want_err else None)
+    else:
+        rc = lib().orc_encode_image_bc7_ex(a.ctypes.data, w, h, s, c, first_row, num_rows, threads, quality,
+                                           mode_mask, shake_ranks, out.ctypes.data,
+                                           err.ctypes.data if want_err else None)
     if rc != 0:
         raise RuntimeError(f"oracle encode failed ({rc})")
     return (out, err) if want_err else out
@@ -155,6 +178,21 @@ def encode_image_bc7enc(img: np.ndarray, fast: bool = False, perceptual: bool = 
     s, h, w, c = a.shape
     out = np.zeros((s * ((h + 3) // 4) * ((w + 3) // 4), 16), np.uint8)
     if lib().orc_encode_image_bc7enc(a.ctypes.data, w, h, s, c, int(fast), int(perceptual), out.ctypes.data) != 0:
+        raise RuntimeError("oracle bc7enc16 encode failed")
+    return out
+
+
+def encode_image_bc7enc_rows(img: np.ndarray, first_row: int, num_rows: int, threads: int = 0, fast: bool = False,
+                             perceptual: bool = True) -> np.ndarray:
+    """bc7enc16 on a block-row range through the oracle's thread pool (CPU baseline)."""
+    a = np.ascontiguousarray(img, dtype=np.uint8)
+    if a.ndim == 3:
+        a = a[None]
+    s, h, w, c = a.shape
+    out = np.zeros((s * num_rows * ((w + 3) // 4), 16), np.uint8)
+    threads = threads or min(os.cpu_count() or 1, 16)
+    if lib().orc_encode_image_bc7enc_rows(a.ctypes.data, w, h, s, c, first_row, num_rows, threads, int(fast),
+                                          int(perceptual), out.ctypes.data) != 0:
         raise RuntimeError("oracle bc7enc16 encode failed")
     return out
 

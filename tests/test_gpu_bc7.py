@@ -156,6 +156,29 @@ def test_bc7_quality_levels(gpu, quality):
         assert np.array_equal(out, ref), (quality, _mismatch_report(out, ref))
 
 
+@pytest.mark.parametrize("performance,quality", [(0.0, 1.0), (0.1, 1.0), (0.5, 1.0), (0.95, 1.0), (0.0, 0.6),
+                                                 (0.05, 0.3)])
+def test_bc7_performance_levels(gpu, performance, quality):
+    """BC7BlockEncoder performance < 1: blocks whose range exceeds 255 *
+    performance quantise with the exhaustive optQuantTrace_d (trace tables of
+    traceBuilder) instead of optQuantAnD_d -- single-index modes with at most 8
+    clusters and both halves of modes 4/5 (amd_bc7_body.cpp:606-633,
+    :1103-1154) -- bit-identical to the oracle's restatement."""
+    import torch
+    g1 = synth.g1(64, 16)
+    noise = synth.noise_rgba(32, 16, seed=9, alpha=True)
+    for img in (g1, noise):
+        src = torch.from_numpy(np.ascontiguousarray(img)[None]).cuda()
+        h, w = img.shape[:2]
+        nb = ((w + 3) // 4) * ((h + 3) // 4)
+        dst = torch.zeros(nb * 16, dtype=torch.uint8, device="cuda")
+        gic.encode_device(7, src, w, h, 1, 4, dst, gic.Options(bc7_quality=quality, bc7_performance=performance))
+        torch.cuda.synchronize()
+        out = dst.cpu().numpy().reshape(-1, 16)
+        ref = oracle_lib.encode_image_bc7(img, quality=quality, performance=performance)
+        assert np.array_equal(out, ref), (performance, _mismatch_report(out, ref))
+
+
 def test_bc7_8k_whole_image_properties(gpu):
     """Config 4 at full size (8192^2 G1): every block decodes, only modes 0-5
     appear (opaque non-solid blocks drop 6/7, Q4), the decoded image is close
