@@ -360,10 +360,16 @@ def bc7enc16_leg(args, gic, src, size, world, dev, rank, fast):
         import oracle_lib
         host = src.cpu().numpy()[0]
         threads = _cpu_threads()
-        rows = 4 if not fast else 16
+        rows = 4
         c0 = time.perf_counter()
         ref = oracle_lib.encode_image_bc7enc_rows(host, 0, rows, threads=threads, fast=fast, perceptual=True)
         dt = time.perf_counter() - c0
+        budget = args.cpu_seconds / 2   # grow the sample to ~budget s of CPU work, bounded by the image
+        if dt < budget / 4:
+            rows = int(min(by, max(rows, rows * budget / max(dt, 1e-3))))
+            c0 = time.perf_counter()
+            ref = oracle_lib.encode_image_bc7enc_rows(host, 0, rows, threads=threads, fast=fast, perceptual=True)
+            dt = time.perf_counter() - c0
         got = dst.cpu().numpy().reshape(-1, 16)[:rows * bx]
         res["cpu_baseline"] = {"value": round(rows * 4 * size / dt / 1e6, 4), "unit": "Mpixels/s", "cores": threads,
                                "kind": "port", "cpu_model": cpu_model(),

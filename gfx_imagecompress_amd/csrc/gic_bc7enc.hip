@@ -116,8 +116,16 @@ __device__ __forceinline__ void ycc(int r, int g, int b, int &l, int &cr, int &c
 // weighted squared distance w0 d0^2 + w1 d1^2 + w2 d2^2 [+ e]
 __device__ __forceinline__ uint32_t wsq(int d0, int d1, int d2, const EncCfg &cf, int e = 0)
 {
-    return (uint32_t)e + __umul24(cf.w[0], (uint32_t)__mul24(d0, d0)) + __umul24(cf.w[1], (uint32_t)__mul24(d1, d1)) +
-           __umul24(cf.w[2], (uint32_t)__mul24(d2, d2));
+    // |d| <= 946 and w <= 512 (see above): tell the optimiser, so that every
+    // product is a 24-bit multiply without masking
+    __builtin_assume((uint32_t)(d0 + 1024) < 2048u);
+    __builtin_assume((uint32_t)(d1 + 1024) < 2048u);
+    __builtin_assume((uint32_t)(d2 + 1024) < 2048u);
+    const uint32_t s0 = (uint32_t)(d0 * d0), s1 = (uint32_t)(d1 * d1), s2 = (uint32_t)(d2 * d2);
+    __builtin_assume(s0 < (1u << 20));
+    __builtin_assume(s1 < (1u << 20));
+    __builtin_assume(s2 < (1u << 20));
+    return (uint32_t)e + __umul24(cf.w[0], s0) + __umul24(cf.w[1], s1) + __umul24(cf.w[2], s2);
 }
 
 // compute_color_distance_rgb with perceptual = true, from the two colours' transforms
