@@ -135,54 +135,97 @@ __device__ __forceinline__ uint32_t ycc_err(int l1, int cr1, int cb1, int l2, in
     return wsq((l1 - l2) >> 8, (cr1 - cr2) >> 8, (cb1 - cb2) >> 8, cf, e);
 }
 
-// evaluate_solution :405-572.  Masked-out texels are computed and discarded
-// (branch-free); the integer totals do not depend on summation order.
-template <bool P>
-__device__ __forceinline__ void evaluate(uint32_t lo, uint32_t hi, uint32_t pb0, uint32_t pb1, const Prob &pr, const uint32_t px[16],
-                         const Ycc &tx, const EncCfg &cf, Res &r)
+// The search below runs K subset problems in lockstep: K = 1 is one problem on
+// pr[0].mask (mode 6, the whole block), K = 2 the two subsets of a mode-1
+// partition (m0 = the texels of subset 0).  Every per-texel pass scores each
+// texel against its own subset's candidate, so mode 1's two subsets share
+// their passes over the block.
+template <int K>
+__device__ __forceinline__ bool first_subset(uint32_t m0, int i)
 {
-    const uint32_t p1 = pr.mode1 ? pb0 : pb1;
-    uint32_t qlo = 0, qhi = 0;
+    return K == 1 || ((m0 >> i) & 1u);
+}
+
+__device__ __forceinline__ uint64_t nibble_mask(uint32_t m)
+{
+    uint64_t r = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        qlo |= ((ch(lo, k) << 1) | pb0) << (8 * k);
-        qhi |= ((ch(hi, k) << 1) | p1) << (8 * k);
+    for (int i = 0; i < 16; ++i) r |= (uint64_t)(((m >> i) & 1u) ? 15u : 0u) << (4 * i);
+    return r;
+}
+
+// evaluate_solution :405-572 for the candidates (lo, hi, pb) of the K problems;
+// a problem's result is updated only if want[s] (find_optimal_solution's
+// changed-endpoints test).  Texels outside a K = 1 problem's mask are computed
+// and discarded (branch-free); the integer totals do not depend on order.
+template <bool P, int K>
+__device__ __forceinline__ void evaluate(const uint32_t lo[K], const uint32_t hi[K], const uint32_t pb0[K],
+                                         const uint32_t pb1[K], const bool want[K], const Prob pr[K], uint32_t m0,
+                                         const uint32_t px[16], const Ycc &tx, const EncCfg &cf, Res r[K])
+{
+    uint32_t a[K], b[K];
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+        const uint32_t p1 = pr[s].mode1 ? pb0[s] : pb1[s];
+        uint32_t qlo = 0, qhi = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            qlo |= ((ch(lo[s], k) << 1) | pb0[s]) << (8 * k);
+            qhi |= ((ch(hi[s], k) << 1) | p1) << (8 * k);
+        }
+        a[s] = expand(qlo, pr[s].cbits + 1);
+        b[s] = expand(qhi, pr[s].cbits + 1);
     }
-    const uint32_t a = expand(qlo, pr.cbits + 1), b = expand(qhi, pr.cbits + 1);
-    const uint32_t N = pr.nsel;
-    uint32_t tot = 0;
+    const uint32_t N = pr[0].nsel;
+    const bool alpha = K == 1 && pr[0].alpha;   // only mode 6 problems carry alpha
+    const uint32_t mask = K == 1 ? pr[0].mask : 0xffffu;
+    uint32_t tot[K];
+#pragma unroll
+    for (int s = 0; s < K; ++s) tot[s] = 0;
     uint64_t ts = 0;
-    const bool any_alpha = __any(pr.alpha);
-    const int w3 = pr.alpha ? (int)cf.w[3] : 0;
+    const bool any_alpha = __any(alpha);
+    const int w3 = alpha ? (int)cf.w[3] : 0;
     if (!P) {
-        const int ar = ch(a, 0), ag = ch(a, 1), ab = ch(a, 2), aa = ch(a, 3);
-        const int dr = (int)ch(b, 0) - ar, dg = (int)ch(b, 1) - ag, db = (int)ch(b, 2) - ab;
-        const int da = pr.alpha ? (int)ch(b, 3) - aa : 0;
-        const float f = N / (float)(dr * dr + dg * dg + db * db + da * da + .00000125f);
+        int dr[K], dg[K], db[K], da[K];
+        float f[K];
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+            dr[s] = (int)ch(b[s], 0) - (int)ch(a[s], 0);
+            dg[s] = (int)ch(b[s], 1) - (int)ch(a[s], 1);
+            db[s] = (int)ch(b[s], 2) - (int)ch(a[s], 2);
+            da[s] = alpha ? (int)ch(b[s], 3) - (int)ch(a[s], 3) : 0;
+            f[s] = N / (float)(dr[s] * dr[s] + dg[s] * dg[s] + db[s] * db[s] + da[s] * da[s] + .00000125f);
+        }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
+            const bool f0 = first_subset<K>(m0, i);
+            const uint32_t A = f0 ? a[0] : a[K - 1], B = f0 ? b[0] : b[K - 1];
+            const int Dr = f0 ? dr[0] : dr[K - 1], Dg = f0 ? dg[0] : dg[K - 1], Db = f0 ? db[0] : db[K - 1];
+            const float F = f0 ? f[0] : f[K - 1];
             const uint32_t c = tex(px, i);
             const int cr = ch(c, 0), cg = ch(c, 1), cb = ch(c, 2), ca = ch(c, 3);
-            int dot = (cr - ar) * dr + (cg - ag) * dg + (cb - ab) * db;
-            if (pr.alpha) dot += (ca - aa) * da;
-            int s = (int)((float)dot * f + .5f);
-            s = clampi_r(s, 1, (int)N - 1);
-            const uint32_t w0 = bc7w(s - 1, N), w1 = bc7w(s, N);
+            int dot = (cr - (int)ch(A, 0)) * Dr + (cg - (int)ch(A, 1)) * Dg + (cb - (int)ch(A, 2)) * Db;
+            if (alpha) dot += (ca - (int)ch(A, 3)) * da[0];
+            int sl = (int)((float)dot * F + .5f);
+            sl = clampi_r(sl, 1, (int)N - 1);
+            const uint32_t w0 = bc7w(sl - 1, N), w1 = bc7w(sl, N);
             int ea0 = 0, ea1 = 0;
             if (any_alpha) {   // wave-uniform: skipped by waves of opaque blocks
-                const int d0 = lerp_ch(a, b, 3, w0) - ca, d1 = lerp_ch(a, b, 3, w1) - ca;
+                const int d0 = lerp_ch(A, B, 3, w0) - ca, d1 = lerp_ch(A, B, 3, w1) - ca;
                 ea0 = mad24(mul24(w3, d0), d0, 0);
                 ea1 = mad24(mul24(w3, d1), d1, 0);
             }
             const uint32_t e0 =
-                wsq(lerp_ch(a, b, 0, w0) - cr, lerp_ch(a, b, 1, w0) - cg, lerp_ch(a, b, 2, w0) - cb, cf, ea0);
+                wsq(lerp_ch(A, B, 0, w0) - cr, lerp_ch(A, B, 1, w0) - cg, lerp_ch(A, B, 2, w0) - cb, cf, ea0);
             const uint32_t e1 =
-                wsq(lerp_ch(a, b, 0, w1) - cr, lerp_ch(a, b, 1, w1) - cg, lerp_ch(a, b, 2, w1) - cb, cf, ea1);
+                wsq(lerp_ch(A, B, 0, w1) - cr, lerp_ch(A, B, 1, w1) - cg, lerp_ch(A, B, 2, w1) - cb, cf, ea1);
             // both reference branches move down exactly when err0 < err1 (:479, :508)
             const bool down = e0 < e1;
-            const bool in = (pr.mask >> i) & 1u;
-            tot += in ? (down ? e0 : e1) : 0u;
-            ts |= (uint64_t)(in ? (uint32_t)(s - down) : 0u) << (4 * i);
+            const uint32_t e = down ? e0 : e1;
+            const bool in = (mask >> i) & 1u;
+            tot[0] += (in && f0) ? e : 0u;
+            if (K == 2) tot[K - 1] += f0 ? 0u : e;
+            ts |= (uint64_t)(in ? (uint32_t)(sl - down) : 0u) << (4 * i);
         }
     } else {
         // ramp point outer (a real loop), texels inner.  Each texel keeps the
@@ -194,52 +237,63 @@ __device__ __forceinline__ void evaluate(uint32_t lo, uint32_t hi, uint32_t pb0,
 #pragma unroll 1
         for (uint32_t j = 0; j < N; ++j) {
             const uint32_t w = bc7w(j, N);
-            int l1, cr1, cb1;
-            ycc(lerp_ch(a, b, 0, w), lerp_ch(a, b, 1, w), lerp_ch(a, b, 2, w), l1, cr1, cb1);
-            const int a1 = lerp_ch(a, b, 3, w);
-            if (any_alpha) {   // wave-uniform
+            int l1[K], cr1[K], cb1[K];
+#pragma unroll
+            for (int s = 0; s < K; ++s)
+                ycc(lerp_ch(a[s], b[s], 0, w), lerp_ch(a[s], b[s], 1, w), lerp_ch(a[s], b[s], 2, w), l1[s], cr1[s],
+                    cb1[s]);
+            if (any_alpha) {   // wave-uniform; K == 1
+                const int a1 = lerp_ch(a[0], b[0], 3, w);
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     const int d = a1 - (int)ch(tex(px, i), 3);
-                    const uint32_t e = ycc_err(l1, cr1, cb1, tx.l[i], tx.cr[i], tx.cb[i], cf, mad24(mul24(w3, d), d, 0));
+                    const uint32_t e = ycc_err(l1[0], cr1[0], cb1[0], tx.l[i], tx.cr[i], tx.cb[i], cf,
+                                               mad24(mul24(w3, d), d, 0));
                     key[i] = min(key[i], (e << 4) | j);
                 }
             } else {
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    const uint32_t e = ycc_err(l1, cr1, cb1, tx.l[i], tx.cr[i], tx.cb[i], cf);
+                    const bool f0 = first_subset<K>(m0, i);
+                    const uint32_t e = ycc_err(f0 ? l1[0] : l1[K - 1], f0 ? cr1[0] : cr1[K - 1],
+                                               f0 ? cb1[0] : cb1[K - 1], tx.l[i], tx.cr[i], tx.cb[i], cf);
                     key[i] = min(key[i], (e << 4) | j);
                 }
             }
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            const bool in = (pr.mask >> i) & 1u;
-            tot += in ? key[i] >> 4 : 0u;
+            const bool f0 = first_subset<K>(m0, i);
+            const bool in = (mask >> i) & 1u;
+            tot[0] += (in && f0) ? key[i] >> 4 : 0u;
+            if (K == 2) tot[K - 1] += f0 ? 0u : key[i] >> 4;
             ts |= (uint64_t)(in ? key[i] & 15u : 0u) << (4 * i);
         }
     }
-    if (tot < r.err) {
-        r.err = tot;
-        r.lo = lo;
-        r.hi = hi;
-        r.pb0 = pb0;
-        r.pb1 = pb1;
-        r.sel = ts;
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+        if (want[s] && tot[s] < r[s].err) {
+            r[s].err = tot[s];
+            r[s].lo = lo[s];
+            r[s].hi = hi[s];
+            r[s].pb0 = pb0[s];
+            r[s].pb1 = pb1[s];
+            r[s].sel = ts & nibble_mask(K == 1 ? mask : (s == 0 ? m0 : ~m0 & 0xffffu));
+        }
     }
 }
 
-// find_optimal_solution :606-729 (modes 1 and 6 both carry p-bits) with
-// fixDegenerateEndpoints :574-604 (mode 1)
-template <bool P>
-__device__ __forceinline__ void fit(float xl[4], float xh[4], const Prob &pr, const uint32_t px[16], const Ycc &tx, const EncCfg &cf, Res &r)
+// find_optimal_solution :606-729, the endpoint quantisation (modes 1 and 6
+// both carry p-bits) with fixDegenerateEndpoints :574-604 (mode 1)
+__device__ __forceinline__ void quantize(float xl[4], float xh[4], const Prob &pr, uint32_t &bmin, uint32_t &bmax,
+                                         uint32_t &bp0, uint32_t &bp1)
 {
 #pragma unroll
     for (int k = 0; k < 4; ++k) xl[k] = sat(xl[k]), xh[k] = sat(xh[k]);
     const int iscalep = (1 << (pr.cbits + 1)) - 1;
     const float scalep = (float)iscalep;
     const uint32_t nb = pr.cbits + 1;
-    uint32_t bmin = 0, bmax = 0, bp0 = 0, bp1 = 0;
+    bmin = bmax = bp0 = bp1 = 0;
     if (!pr.mode1) {
         float be0 = 1e+9f, be1 = 1e+9f;
 #pragma unroll
@@ -305,42 +359,76 @@ __device__ __forceinline__ void fit(float xl[4], float xh[4], const Prob &pr, co
             bmax = (bmax & ~(0xffu << (8 * k))) | (mx << (8 * k));
         }
     }
-    if (r.err == kNone || bmin != r.lo || bmax != r.hi || bp0 != r.pb0 || bp1 != r.pb1)
-        evaluate<P>(bmin, bmax, bp0, bp1, pr, px, tx, cf, r);
 }
 
-// compute_least_squares_endpoints_rgb / _rgba :197-280, then the 1/255 scale
-__device__ __forceinline__ void lsq(const Prob &pr, uint64_t sel, const uint32_t px[16], const EncLds &L, float xl[4], float xh[4])
+// find_optimal_solution for the K problems: quantise each active one's
+// endpoints, evaluate those that differ from its best (:710, :724)
+template <bool P, int K>
+__device__ __forceinline__ void fit(float xl[K][4], float xh[K][4], const bool active[K], const Prob pr[K],
+                                    uint32_t m0, const uint32_t px[16], const Ycc &tx, const EncCfg &cf, Res r[K])
 {
-    const float *wx = L.wx + (pr.nsel == 16 ? 32 : 0);
-    float z00 = 0.0f, z10 = 0.0f, z11 = 0.0f;
-    float q00[4] = {0.f, 0.f, 0.f, 0.f}, t[4] = {0.f, 0.f, 0.f, 0.f};
+    uint32_t lo[K], hi[K], p0[K], p1[K];
+    bool want[K], any = false;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {   // texel order; texels outside the subset leave every sum as it is
-        const bool in = (pr.mask >> i) & 1u;
+    for (int s = 0; s < K; ++s) {
+        quantize(xl[s], xh[s], pr[s], lo[s], hi[s], p0[s], p1[s]);
+        want[s] = active[s] && (r[s].err == kNone || lo[s] != r[s].lo || hi[s] != r[s].hi || p0[s] != r[s].pb0 ||
+                                p1[s] != r[s].pb1);
+        any = any || want[s];
+    }
+    if (any) evaluate<P, K>(lo, hi, p0, p1, want, pr, m0, px, tx, cf, r);
+}
+
+// compute_least_squares_endpoints_rgb / _rgba :197-280 for the K problems in
+// one texel pass (each texel adds to its own subset's sums, in texel order),
+// then the 1/255 scale
+template <int K>
+__device__ __forceinline__ void lsq(const Prob pr[K], uint32_t m0, uint64_t sel, const uint32_t px[16],
+                                    const EncLds &L, float xl[K][4], float xh[K][4])
+{
+    const float *wx = L.wx + (pr[0].nsel == 16 ? 32 : 0);
+    float z00[K], z10[K], z11[K], q00[K][4], t[K][4];
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+        z00[s] = z10[s] = z11[s] = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q00[s][k] = t[s][k] = 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const bool f0 = first_subset<K>(m0, i);
+        const bool in = K == 2 || ((pr[0].mask >> i) & 1u);
         const float *w4 = wx + 4 * sel_at(sel, i);
-        z00 = in ? z00 + w4[0] : z00;
-        z10 = in ? z10 + w4[1] : z10;
-        z11 = in ? z11 + w4[2] : z11;
         const float w = w4[3];
+        const uint32_t c = tex(px, i);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float c = (float)ch(tex(px, i), k);
-            q00[k] = in ? q00[k] + w * c : q00[k];
-            t[k] = in ? t[k] + c : t[k];
+        for (int s = 0; s < K; ++s) {
+            const bool add = in && (s == 0 ? f0 : !f0);
+            z00[s] = add ? z00[s] + w4[0] : z00[s];
+            z10[s] = add ? z10[s] + w4[1] : z10[s];
+            z11[s] = add ? z11[s] + w4[2] : z11[s];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float v = (float)ch(c, k);
+                q00[s][k] = add ? q00[s][k] + w * v : q00[s][k];
+                t[s][k] = add ? t[s][k] + v : t[s][k];
+            }
         }
     }
-    const float z01 = z10;
-    float det = z00 * z11 - z01 * z10;
-    if (det != 0.0f) det = 1.0f / det;
-    const float i00 = z11 * det, i01 = -z01 * det, i10 = -z10 * det, i11 = z00 * det;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const float q10 = t[k] - q00[k];
-        float l = i00 * q00[k] + i01 * q10, h = i10 * q00[k] + i11 * q10;
-        if (k == 3 && !pr.alpha) l = h = 255.0f;
-        xl[k] = l * (1.0f / 255.0f);
-        xh[k] = h * (1.0f / 255.0f);
+    for (int s = 0; s < K; ++s) {
+        const float z01 = z10[s];
+        float det = z00[s] * z11[s] - z01 * z10[s];
+        if (det != 0.0f) det = 1.0f / det;
+        const float i00 = z11[s] * det, i01 = -z01 * det, i10 = -z10[s] * det, i11 = z00[s] * det;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float q10 = t[s][k] - q00[s][k];
+            float l = i00 * q00[s][k] + i01 * q10, h = i10 * q00[s][k] + i11 * q10;
+            if (k == 3 && !pr[s].alpha) l = h = 255.0f;
+            xl[s][k] = l * (1.0f / 255.0f);
+            xh[s][k] = h * (1.0f / 255.0f);
+        }
     }
 }
 
@@ -386,26 +474,12 @@ __device__ __forceinline__ void one_colour(uint32_t cr, uint32_t cg, uint32_t cb
     r.err = tot;
 }
 
-// color_cell_compression :731-1024
+// color_cell_compression :756-874: the subset's mean and principal axis, and the
+// PCA endpoints the first fit starts from
 template <bool P>
-__device__ __forceinline__ Res cell(const Prob &pr, const uint32_t px[16], const Ycc &tx, const EncCfg &cf, const EncLds &L)
+__device__ __forceinline__ void pca_endpoints(const Prob &pr, const uint32_t px[16], float cmin[4], float cmax[4],
+                                              float mn[4])
 {
-    Res r;
-    r.err = kNone;
-    r.lo = r.hi = r.pb0 = r.pb1 = 0;
-    r.sel = 0;
-    if (pr.mode1) {   // the subset is one colour: pack it directly (:738-754)
-        uint32_t first = 0;
-        bool same = true;
-#pragma unroll
-        for (int i = 15; i >= 0; --i) first = ((pr.mask >> i) & 1u) ? tex(px, i) & 0xffffffu : first;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) same = same && (!((pr.mask >> i) & 1u) || (tex(px, i) & 0xffffffu) == first);
-        if (same) {
-            one_colour<P>(ch(first, 0), ch(first, 1), ch(first, 2), pr, px, tx, cf, L, r);
-            return r;
-        }
-    }
     // mean and principal axis (:756-841)
     float m[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -414,7 +488,7 @@ __device__ __forceinline__ Res cell(const Prob &pr, const uint32_t px[16], const
 #pragma unroll
         for (int k = 0; k < 4; ++k) m[k] = in ? m[k] + (float)ch(tex(px, i), k) : m[k];
     }
-    float ms[4], mn[4], ax[4] = {0.f, 0.f, 0.f, 0.f};
+    float ms[4], ax[4] = {0.f, 0.f, 0.f, 0.f};
     const float inv_n = 1.0f / (float)pr.n, inv_n255 = 1.0f / (float)(pr.n * 255.0f);
 #pragma unroll
     for (int k = 0; k < 4; ++k) ms[k] = m[k] * inv_n, mn[k] = sat(m[k] * inv_n255);
@@ -504,7 +578,6 @@ __device__ __forceinline__ Res cell(const Prob &pr, const uint32_t px[16], const
     }
     lo *= (1.0f / 255.0f);
     hi *= (1.0f / 255.0f);
-    float cmin[4], cmax[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) cmin[k] = sat(mn[k] + ax[k] * lo), cmax[k] = sat(mn[k] + ax[k] * hi);
     if (cmin[0] * 1.0f + cmin[1] * 1.0f + cmin[2] * 1.0f + cmin[3] * 1.0f >
@@ -517,6 +590,37 @@ __device__ __forceinline__ Res cell(const Prob &pr, const uint32_t px[16], const
         }
     }
 
+}
+
+// color_cell_compression :731-1024 for K problems in lockstep
+template <bool P, int K>
+__device__ __forceinline__ void cells(const Prob pr[K], uint32_t m0, const uint32_t px[16], const Ycc &tx,
+                                      const EncCfg &cf, const EncLds &L, Res r[K])
+{
+    bool fin[K];   // the subset was packed as one colour (:738-754): no trials
+    float cmin[K][4], cmax[K][4], mn[K][4];
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+        r[s].err = kNone;
+        r[s].lo = r[s].hi = r[s].pb0 = r[s].pb1 = 0;
+        r[s].sel = 0;
+        fin[s] = false;
+        if (pr[s].mode1) {
+            uint32_t first = 0;
+            bool same = true;
+#pragma unroll
+            for (int i = 15; i >= 0; --i) first = ((pr[s].mask >> i) & 1u) ? tex(px, i) & 0xffffffu : first;
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                same = same && (!((pr[s].mask >> i) & 1u) || (tex(px, i) & 0xffffffu) == first);
+            if (same) {
+                one_colour<P>(ch(first, 0), ch(first, 1), ch(first, 2), pr[s], px, tx, cf, L, r[s]);
+                fin[s] = true;
+            }
+        }
+        if (!fin[s]) pca_endpoints<P>(pr[s], px, cmin[s], cmax[s], mn[s]);
+    }
+
     // Trials, each a fit that keeps the best (:874-1006): t = 0 the PCA endpoints;
     // then the least-squares refit of the current selectors; uber >= 1: refits of
     // the snapshot with its minimum selectors raised, its maximum lowered, both;
@@ -527,44 +631,61 @@ __device__ __forceinline__ Res cell(const Prob &pr, const uint32_t px[16], const
     const int Q = cf.uber >= 4 ? (int)cf.uber - 2 : 1;
     const int ngrid = cf.uber >= 2 ? (Q + 2) * (Q + 2) - 1 : 0;
     const int ntr = 1 + nls + nub + ngrid;
-    const int maxs = (int)pr.nsel - 1;
-    bool zero = false, grid = false;
+    const int maxs = (int)pr[0].nsel - 1;
+    bool zero[K], grid[K];
+    uint32_t smin[K], smax[K];
     uint64_t base = 0;
-    uint32_t smin = 16, smax = 0;
+#pragma unroll
+    for (int s = 0; s < K; ++s) zero[s] = grid[s] = false, smin[s] = 16, smax[s] = 0;
     for (int t = 0; t < ntr; ++t) {
-        if (zero) break;   // color_cell_compression returns 0 at once
-        if (t == 1 + nls) {
-            base = r.sel;
-            smin = 16, smax = 0;
+        if (t == 1 + nls) {   // the uber snapshot: each subset's selectors sit in its own nibbles
+            base = 0;
+#pragma unroll
+            for (int s = 0; s < K; ++s) base |= r[s].sel;
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const bool in = (pr.mask >> i) & 1u;
-                const uint32_t s = sel_at(base, i);
-                smin = in && s < smin ? s : smin;
-                smax = in && s > smax ? s : smax;
+                const bool f0 = first_subset<K>(m0, i);
+                const uint32_t v = sel_at(base, i);
+#pragma unroll
+                for (int s = 0; s < K; ++s) {
+                    const bool mine = (s == 0 ? f0 : !f0) && (K == 2 || ((pr[0].mask >> i) & 1u));
+                    smin[s] = mine && v < smin[s] ? v : smin[s];
+                    smax[s] = mine && v > smax[s] ? v : smax[s];
+                }
             }
         }
-        if (t == 1 + nls + nub) grid = r.err > ((pr.n * 56u) >> 4);
-        if (t >= 1 + nls + nub && !grid) break;
-        float xl[4], xh[4];
+        bool active[K], any = false;
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+            if (t == 1 + nls + nub) grid[s] = r[s].err > ((pr[s].n * 56u) >> 4);
+            active[s] = !fin[s] && !zero[s] && (t < 1 + nls + nub || grid[s]);
+            any = any || active[s];
+        }
+        if (!any) break;   // color_cell_compression returned (0) or finished its trials
+        float xl[K][4], xh[K][4];
         if (t == 0) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) xl[k] = cmin[k], xh[k] = cmax[k];
+            for (int s = 0; s < K; ++s)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) xl[s][k] = cmin[s][k], xh[s][k] = cmax[s][k];
         } else {
             uint64_t ts = 0;
             if (t <= nls) {
-                ts = r.sel;
+#pragma unroll
+                for (int s = 0; s < K; ++s) ts |= r[s].sel;
             } else if (t < 1 + nls + nub) {
-                // texels outside the subset get some selector in 0..15 that lsq ignores
+                // texels outside the problems get some selector in 0..15 that lsq ignores
                 const int u = t - 1 - nls;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    uint32_t s = sel_at(base, i);
-                    if (u != 1 && s == smin && s < pr.nsel - 1)
-                        s++;
-                    else if (u != 0 && s == smax && s > 0)
-                        s--;
-                    ts |= (uint64_t)s << (4 * i);
+                    const bool f0 = first_subset<K>(m0, i);
+                    const uint32_t lo_s = f0 ? smin[0] : smin[K - 1], hi_s = f0 ? smax[0] : smax[K - 1];
+                    uint32_t v = sel_at(base, i);
+                    if (u != 1 && v == lo_s && v < pr[0].nsel - 1)
+                        v++;
+                    else if (u != 0 && v == hi_s && v > 0)
+                        v--;
+                    ts |= (uint64_t)v << (4 * i);
                 }
             } else {
                 int g = t - (1 + nls + nub);
@@ -577,18 +698,21 @@ __device__ __forceinline__ Res cell(const Prob &pr, const uint32_t px[16], const
                     ts |= (uint64_t)(uint32_t)clampf_r(v, 0, (float)maxs) << (4 * i);
                 }
             }
-            lsq(pr, ts, px, L, xl, xh);
+            lsq<K>(pr, m0, ts, px, L, xl, xh);
         }
-        fit<P>(xl, xh, pr, px, tx, cf, r);
-        zero = r.err == 0;
+        fit<P, K>(xl, xh, active, pr, m0, px, tx, cf, r);
+#pragma unroll
+        for (int s = 0; s < K; ++s) zero[s] = zero[s] || (active[s] && r[s].err == 0);
     }
-    if (!zero && pr.mode1) {   // the subset mean as one colour (:1009-1021)
-        Res avg = r;
-        one_colour<P>((uint32_t)(int)(.5f + mn[0] * 255.0f), (uint32_t)(int)(.5f + mn[1] * 255.0f),
-                      (uint32_t)(int)(.5f + mn[2] * 255.0f), pr, px, tx, cf, L, avg);
-        if (avg.err < r.err) r = avg;
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+        if (pr[s].mode1 && !fin[s] && !zero[s]) {   // the subset mean as one colour (:1009-1021)
+            Res avg = r[s];
+            one_colour<P>((uint32_t)(int)(.5f + mn[s][0] * 255.0f), (uint32_t)(int)(.5f + mn[s][1] * 255.0f),
+                          (uint32_t)(int)(.5f + mn[s][2] * 255.0f), pr[s], px, tx, cf, L, avg);
+            if (avg.err < r[s].err) r[s] = avg;
+        }
     }
-    return r;
 }
 
 // color_cell_compression_est :1026-1162 for both subsets of a two-subset shape
@@ -781,34 +905,30 @@ __device__ __forceinline__ uint4 encode_block(const uint32_t px[16], const EncCf
     bool alpha = false;
 #pragma unroll
     for (int i = 0; i < 16; ++i) alpha = alpha || (tex(px, i) >> 24) < 255u;
-    Res r6, s0, s1;
-    s0.err = s1.err = kNone;
+    Res r6[1], r1[2];
     bool mode1 = false;
-    uint32_t part = 0, m0 = 0xffffu;
-    // problem 0: mode 6 on the block; 1, 2: the two subsets of mode 1's partition
-    for (int prob = 0; prob < 3; ++prob) {
-        Prob pr;
-        if (prob == 0) {
-            pr.mask = 0xffffu, pr.n = 16, pr.nsel = 16, pr.cbits = 7, pr.mode1 = false, pr.alpha = alpha;
-        } else {
-            if (alpha || r6.err == 0 || cf.max_parts == 0) break;
-            if (prob == 1) {
-                part = pick_partition<P>(px, tx, cf);
-                m0 = shape_mask(kBc7Shape2[part], 0);
-            } else if (s0.err > r6.err) {
-                break;   // the reference stops once the first subset alone loses
-            }
-            pr.mask = prob == 1 ? m0 : (~m0 & 0xffffu);
-            pr.n = (uint32_t)__popc(pr.mask), pr.nsel = 8, pr.cbits = 6, pr.mode1 = true, pr.alpha = false;
-        }
-        const Res r = cell<P>(pr, px, tx, cf, L);
-        if (prob == 0)
-            r6 = r;
-        else if (prob == 1)
-            s0 = r;
-        else if (s0.err + r.err < r6.err)
-            mode1 = true, s1 = r;
+    uint32_t part = 0;
+    {   // mode 6 on the whole block
+        Prob p6[1];
+        p6[0].mask = 0xffffu, p6[0].n = 16, p6[0].nsel = 16, p6[0].cbits = 7, p6[0].mode1 = false, p6[0].alpha = alpha;
+        cells<P, 1>(p6, 0xffffu, px, tx, cf, L, r6);
     }
+    if (!alpha && r6[0].err > 0 && cf.max_parts > 0) {
+        // mode 1 on the partition the estimator picks, both subsets at once (the
+        // reference stops after the first subset if it alone loses: equivalent)
+        part = pick_partition<P>(px, tx, cf);
+        const uint32_t m0 = shape_mask(kBc7Shape2[part], 0);
+        Prob p1[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            p1[k].mask = k ? (~m0 & 0xffffu) : m0;
+            p1[k].n = (uint32_t)__popc(p1[k].mask), p1[k].nsel = 8, p1[k].cbits = 6, p1[k].mode1 = true;
+            p1[k].alpha = false;
+        }
+        cells<P, 2>(p1, m0, px, tx, cf, L, r1);
+        mode1 = r1[0].err + r1[1].err < r6[0].err;
+    }
+    const Res s0 = r1[0], s1 = r1[1];
     uint32_t lo[2], hi[2], pb[2][2];
     uint64_t sel;
     if (mode1) {
@@ -816,8 +936,8 @@ __device__ __forceinline__ uint4 encode_block(const uint32_t px[16], const EncCf
         lo[0] = s0.lo, hi[0] = s0.hi, pb[0][0] = s0.pb0, pb[0][1] = 0;
         lo[1] = s1.lo, hi[1] = s1.hi, pb[1][0] = s1.pb0, pb[1][1] = 0;
     } else {
-        sel = r6.sel;
-        lo[0] = r6.lo, hi[0] = r6.hi, pb[0][0] = r6.pb0, pb[0][1] = r6.pb1;
+        sel = r6[0].sel;
+        lo[0] = r6[0].lo, hi[0] = r6[0].hi, pb[0][0] = r6[0].pb0, pb[0][1] = r6[0].pb1;
         lo[1] = hi[1] = pb[1][0] = pb[1][1] = 0;
     }
     return pack_block(mode1, part, sel, lo, hi, pb);
