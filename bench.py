@@ -355,6 +355,9 @@ def bc7enc16_leg(args, gic, src, size, world, dev, rank, fast):
            "roofline": {"bound": "valu", "achieved": round(alg / (kern_ms * 1e-3) / 1e9, 3), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(alg / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
                         "alg_bytes_per_launch": alg}}
+    valu = _valu_roofline("valu_bc7enc16_fast.json" if fast else "valu_bc7enc16.json", size, size, kern_ms)
+    if valu is not None:
+        res["roofline"]["valu"] = valu
     if rank == 0 and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib
@@ -377,6 +380,26 @@ def bc7enc16_leg(args, gic, src, size, world, dev, rank, fast):
         res["gpu_parity"] = "bit-exact" if np.array_equal(got, ref) else \
             f"{int((got != ref).any(axis=1).sum())} blocks differ"
     return res
+
+
+def _valu_roofline(name, size, rows, kern_ms):
+    """VALU issue roofline of a kernel: SQ_INSTS_VALU per launch from the
+    committed PMC summary profiles/<name> (tools/valu_json.py, same workload)
+    over this run's measured launch duration; None when absent or for another
+    workload size."""
+    vj = os.path.join(ROOT, "profiles", name)
+    try:
+        with open(vj) as f:
+            vr = json.load(f)
+        if vr.get("size") != size or vr.get("rows") != rows:
+            return None
+        rate = vr["valu_insts_per_launch"] / (kern_ms * 1e-3)
+        return {"bound": "valu", "achieved": round(rate / 1e12, 4), "peak": round(VALU_PEAK / 1e12, 4),
+                "unit": "T wave-instr/s", "frac": round(rate / VALU_PEAK, 4),
+                "insts_per_launch": vr["valu_insts_per_launch"], "kernel": vr.get("kernel", "")[:60],
+                "source": os.path.relpath(vj, ROOT)}
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def _cpu_threads():
@@ -562,20 +585,7 @@ def main():
     # VALU issue roofline of the same kernel: SQ_INSTS_VALU per launch from the
     # committed PMC summary (tools/pmc_valu.sh + tools/valu_json.py, same
     # workload) over this run's measured launch duration
-    valu = None
-    vj = os.path.join(ROOT, "profiles", f"valu_{args.format}.json")
-    if os.path.exists(vj):
-        try:
-            with open(vj) as f:
-                vr = json.load(f)
-            if vr.get("size") == size and vr.get("rows") == rows * 4:
-                rate = vr["valu_insts_per_launch"] / (kern_ms * 1e-3)
-                valu = {"bound": "valu", "achieved": round(rate / 1e12, 4), "peak": round(VALU_PEAK / 1e12, 4),
-                        "unit": "T wave-instr/s", "frac": round(rate / VALU_PEAK, 4),
-                        "insts_per_launch": vr["valu_insts_per_launch"], "kernel": vr.get("kernel", "")[:60],
-                        "source": os.path.relpath(vj, ROOT)}
-        except (OSError, ValueError, KeyError):
-            valu = None
+    valu = _valu_roofline(f"valu_{args.format}.json", size, rows * 4, kern_ms)
 
     bc7 = bc7_pruned = None
     if fmt == 1 and args.bc7_rows != 0:

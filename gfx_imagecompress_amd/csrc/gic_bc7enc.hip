@@ -945,6 +945,11 @@ __device__ __forceinline__ uint4 encode_block(const uint32_t px[16], const EncCf
 
 // ---- kernels ---------------------------------------------------------------
 
+// waves per SIMD the kernels are register-budgeted for (build-time override for studies)
+#ifndef GIC_ENC_WAVES
+#define GIC_ENC_WAVES 2
+#endif
+
 __device__ __forceinline__ void load_tables(EncLds &L)
 {
     for (uint32_t i = threadIdx.x; i < 96; i += blockDim.x)
@@ -956,7 +961,7 @@ __device__ __forceinline__ void load_tables(EncLds &L)
 // Image_CompressRichGel999BC7 :21-71 over 8-bit texels (its float round trip
 // v/255.0f -> R8G8B8A8_UNORM gives back the bytes)
 template <bool P>
-__global__ void __launch_bounds__(256, 2) bc7enc_image_kernel(Geometry g, EncCfg cf, int force_alpha_one,
+__global__ void __launch_bounds__(256, GIC_ENC_WAVES) bc7enc_image_kernel(Geometry g, EncCfg cf, int force_alpha_one,
                                                            uint4 *__restrict__ dst)
 {
     __shared__ EncLds L;
@@ -972,7 +977,7 @@ __global__ void __launch_bounds__(256, 2) bc7enc_image_kernel(Geometry g, EncCfg
 
 // Image_CompressRichGel999BC7enc16 :73-97: blocks of 16 packed RGBA8 words
 template <bool P>
-__global__ void __launch_bounds__(256, 2) bc7enc_blocks_kernel(const uint4 *__restrict__ blocks, uint32_t n, EncCfg cf,
+__global__ void __launch_bounds__(256, GIC_ENC_WAVES) bc7enc_blocks_kernel(const uint4 *__restrict__ blocks, uint32_t n, EncCfg cf,
                                                             uint4 *__restrict__ dst)
 {
     __shared__ EncLds L;
@@ -992,7 +997,7 @@ __global__ void __launch_bounds__(256, 2) bc7enc_blocks_kernel(const uint4 *__re
 // to RGBA8 as saturate(v) * 255 + 0.5 truncated (TinyImageFormat's UNORM8 encode
 // is un-vendored; this rounding is unpinned and is the identity on v / 255.0f)
 template <bool P>
-__global__ void __launch_bounds__(256, 2) bc7enc_f32_kernel(const float *__restrict__ blocks, uint32_t n, EncCfg cf,
+__global__ void __launch_bounds__(256, GIC_ENC_WAVES) bc7enc_f32_kernel(const float *__restrict__ blocks, uint32_t n, EncCfg cf,
                                                          uint4 *__restrict__ dst)
 {
     __shared__ EncLds L;

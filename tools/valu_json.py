@@ -1,6 +1,11 @@
 """Per-launch VALU issue figures of a kernel from a rocprofv3 --pmc csv directory.
 
     python tools/valu_json.py <pmc dir> <kernel substring> <bench json> <out json> [--size S --rows R]
+                              [--skip N --take M --leg KEY]
+
+--skip/--take pick a window of the matching dispatches (two bench legs that
+launch the same kernel template, e.g. bc7enc16 uber 4 then uber 0); --leg takes
+the launch duration from that leg's kernel_ms.
 
 Writes the per-launch SQ_INSTS_VALU (wave instructions, summed over the chip),
 waves, and the VALU issue rate against the gfx950 peak (256 CUs x 4 SIMDs, one
@@ -27,6 +32,9 @@ def main():
     ap.add_argument("--stats", default="")
     ap.add_argument("--size", type=int, default=8192)
     ap.add_argument("--rows", type=int, default=8192)
+    ap.add_argument("--skip", type=int, default=0, help="drop the first N matching dispatches")
+    ap.add_argument("--take", type=int, default=0, help="keep at most N matching dispatches (0 = all)")
+    ap.add_argument("--leg", default="", help="take kernel_ms from this sub-object of the bench line")
     a = ap.parse_args()
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     names = {}
@@ -39,13 +47,17 @@ def main():
             names[d] = r["Kernel_Name"]
     if not per:
         raise SystemExit(f"no dispatch of {a.kernel} in {a.pmc_dir}")
-    disp = sorted(per)
+    disp = sorted(per)[a.skip:]
+    if a.take:
+        disp = disp[:a.take]
     keys = sorted({k for d in disp for k in per[d]})
     avg = {k: sum(per[d][k] for d in disp) / len(disp) for k in keys}
     bench = json.loads(open(a.bench_json).read().strip().splitlines()[-1])
+    if a.leg:
+        bench = bench[a.leg]
     dur_ms = bench["kernel_ms"]
-    src = "bench kernel_ms (HIP events, launch stream)"
-    if a.stats:
+    src = "bench kernel_ms (HIP events, launch stream)" + (f", leg {a.leg}" if a.leg else "")
+    if a.stats and not a.leg:
         for r in csv.DictReader(open(a.stats)):
             if a.kernel in r["Name"]:
                 dur_ms = float(r["AverageNs"]) / 1e6
