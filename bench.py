@@ -67,6 +67,8 @@ def parse():
                    help="with the default BC1 workload, also time BC7 on this many block rows of the same "
                         "texture (-1 = the whole 8K texture, 0 = skip)")
     p.add_argument("--no-bc45", action="store_true", help="skip the BC4/BC5 8K legs (configs[2])")
+    p.add_argument("--bc7-mse-bound", type=float, default=0.5,
+                   help="BC7 bounded-exit legs: per-block MSE under which the probe's block is final (0 = no legs)")
     p.add_argument("--no-bc7enc", action="store_true", help="skip the bc7enc16 (fast BC7 path) legs")
     p.add_argument("--bc7-shake-ranks", type=int, default=2,
                    help="pruned BC7 search leg: partitions shaken per single-index mode (gic_options."
@@ -193,7 +195,7 @@ def _gather_all(dst, world):
     return out_all
 
 
-def bc7_secondary(args, gic, src, size, avail_rows, world, dev, rank, shake_ranks=0, ref_rows=None):
+def bc7_secondary(args, gic, src, size, avail_rows, world, dev, rank, shake_ranks=0, ref_rows=None, bound=0.0):
     """BC7 default quality (configs[3]) on the same texture: one timed pass over
     `--bc7-rows` block rows per rank after a short warm-up, plus (rank 0) the
     CPU restatement on one block row with a bit-exactness check."""
@@ -203,7 +205,7 @@ def bc7_secondary(args, gic, src, size, avail_rows, world, dev, rank, shake_rank
     rows = avail_rows if args.bc7_rows < 0 else min(args.bc7_rows, avail_rows)
     dst = torch.empty(bx * rows * 16, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
-    opts = gic.Options(bc7_quality=args.bc7_quality, bc7_shake_ranks=shake_ranks)
+    opts = gic.Options(bc7_quality=args.bc7_quality, bc7_shake_ranks=shake_ranks, bc7_mse_bound=bound)
     gic.encode_device(7, src, size, size, 1, 4, dst, opts, 0, min(rows, 4), stream=stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -224,6 +226,10 @@ def bc7_secondary(args, gic, src, size, avail_rows, world, dev, rank, shake_rank
     px = size * rows * 4 * world
     search = "exact (reference search, bit-identical)" if shake_ranks == 0 else \
         f"pruned: {shake_ranks} partitions shaken per mode (per-block MSE tolerance)"
+    if bound > 0:
+        search = (f"bounded exit: blocks whose mode-3/mode-1 probe decodes within MSE {bound:g} are final "
+                  f"(contract met by construction), the rest " +
+                  ("the exact search" if shake_ranks == 0 else f"the pruned search ({shake_ranks} partitions)"))
     res = {"metric": f"Mpixels/s BC7 quality {args.bc7_quality:g} (all modes, shakers on), {search}",
            "value": round(px / wall / 1e6, 4), "unit": "Mpixels/s",
            "blocks_per_s": round(bx * rows * world / wall, 1), "ms_per_pass": round(wall * 1e3, 2),
@@ -243,6 +249,8 @@ def bc7_secondary(args, gic, src, size, avail_rows, world, dev, rank, shake_rank
         res["gpu_parity"] = (f"block row 0: {int((got == ref_rows).all(axis=1).sum())}/{bx} bit-identical to the "
                              f"exact oracle, {int((mg > mc * 1.001 + 0.5).sum())} outside the MSE tolerance, "
                              f"mean MSE {mg.mean():.4f} vs {mc.mean():.4f}")
+        if bound > 0:
+            res["gpu_parity"] += f", {int((mg <= bound).sum())}/{bx} within the exit bound"
     elif rank == 0 and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib
@@ -588,11 +596,18 @@ def main():
     valu = _valu_roofline(f"valu_{args.format}.json", size, rows * 4, kern_ms)
 
     bc7 = bc7_pruned = None
+    bounded = {}
     if fmt == 1 and args.bc7_rows != 0:
         bc7 = bc7_secondary(args, gic, src, size, rows, world, dev, rank)
         ref_row = bc7.pop("_ref_row", None)
         if args.bc7_shake_ranks > 0:
             bc7_pruned = bc7_secondary(args, gic, src, size, rows, world, dev, rank, args.bc7_shake_ranks, ref_row)
+        if args.bc7_mse_bound > 0:
+            bounded["bc7_bounded"] = bc7_secondary(args, gic, src, size, rows, world, dev, rank, 0, ref_row,
+                                                   args.bc7_mse_bound)
+            if args.bc7_shake_ranks > 0:
+                bounded["bc7_bounded_pruned"] = bc7_secondary(args, gic, src, size, rows, world, dev, rank,
+                                                              args.bc7_shake_ranks, ref_row, args.bc7_mse_bound)
     enc16 = {}
     if fmt == 1 and not args.no_bc7enc:
         enc16["bc7enc16"] = bc7enc16_leg(args, gic, src, size, world, dev, rank, fast=False)
@@ -648,6 +663,7 @@ def main():
             line["bc7"] = bc7
         if bc7_pruned is not None:
             line["bc7_pruned"] = bc7_pruned
+        line.update(bounded)
         line.update(enc16)
         line.update(bc45)
         print(json.dumps(line), flush=True)

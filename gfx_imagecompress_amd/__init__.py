@@ -59,6 +59,7 @@ class _COptions(ctypes.Structure):
         ("bc7enc_max_partitions", ctypes.c_uint8),
         ("bc7enc_least_squares", ctypes.c_uint8),
         ("bc7enc_filterbank", ctypes.c_uint8),
+        ("bc7_mse_bound", ctypes.c_float),
     ]
 
 
@@ -90,6 +91,8 @@ class Options:
     bc7enc_max_partitions: int = 64
     bc7enc_least_squares: bool = True
     bc7enc_filterbank: bool = True
+    # BC7 bounded exit: blocks whose cheap probe decodes within this MSE are final (0 = off)
+    bc7_mse_bound: float = 0.0
 
     def to_c(self) -> _COptions:
         o = _COptions()
@@ -111,6 +114,7 @@ class Options:
         o.bc7enc_max_partitions = int(self.bc7enc_max_partitions)
         o.bc7enc_least_squares = int(bool(self.bc7enc_least_squares))
         o.bc7enc_filterbank = int(bool(self.bc7enc_filterbank))
+        o.bc7_mse_bound = float(self.bc7_mse_bound)
         return o
 
     @staticmethod

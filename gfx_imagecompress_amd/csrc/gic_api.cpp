@@ -78,6 +78,7 @@ extern "C" void gic_default_options(gic_options *o)
     o->bc7enc_max_partitions = 64;           // richgel999_bc7enc16.h:58
     o->bc7enc_least_squares = 1;
     o->bc7enc_filterbank = 1;
+    o->bc7_mse_bound = 0.f;
 }
 
 extern "C" uint32_t gic_block_bytes(gic_format fmt)
@@ -92,6 +93,7 @@ static int check_options(gic_format fmt, const gic_options &o)
     if (fmt == GIC_FMT_BC4 && o.bc4_channel > 3) return GIC_EINVAL;
     if (o.bc7_performance != o.bc7_performance) return GIC_EINVAL;   // NaN (the reference clamps to [0, 1])
     if (o.bc7_shake_ranks > 8) return GIC_EINVAL;
+    if (!(o.bc7_mse_bound >= 0.f) || o.bc7_mse_bound > 65025.f) return GIC_EINVAL;   // NaN, negative, > 255^2
     if (fmt == GIC_FMT_BC7ENC16 && (o.bc7enc_uber_level > 4 || o.bc7enc_max_partitions > 64)) return GIC_EINVAL;
     return GIC_OK;
 }

@@ -80,7 +80,8 @@ __device__ __forceinline__ int sp_index(int clog, int bits, int v, int o1, int o
 struct BlockMeta {
     uint32_t valid;        // legal-mode mask after CompressBlock's filtering
     uint32_t flags;        // bit0: unsupported (needs optQuantTrace_d), bit1: integral texels,
-                           // bit2: error threshold met (staged low-quality pipeline)
+                           // bit2: error threshold met (staged low-quality pipeline) or
+                           // final after the bounded-exit probe (k_bound)
     double max_range;
 };
 
@@ -1271,6 +1272,11 @@ struct Params {
     // with the least search error (DESIGN.md, BC7 pruned search)
     int decode_select;
     int dual_cap;   // pruned search: dual-index candidates shaken per mode, 2 x bc7_shake_ranks (0 = the reference's gating)
+    // bounded exit (gic_options.bc7_mse_bound > 0): decoded-SSE bound of the
+    // probe stages (64 x the MSE bound), and k_select leaving alone the blocks
+    // the probe finished
+    double bound_sse;
+    int skip_done;
 };
 
 // BlockMeta.flags bit 2: the block met the error threshold in an earlier
@@ -2121,6 +2127,7 @@ __global__ void __launch_bounds__(256) k_select(Params p, Workspace ws, uint4 *_
         }
         return;
     }
+    if (p.skip_done && (meta.flags & 4u)) return;   // written by k_bound
     const int order[8] = {6, 4, 3, 1, 2, 0, 7, 5};
     double best = 1.7976931348623157e308, best_d = 1.7976931348623157e308;
     const float *tex = ws.tex + (size_t)b * 64;
@@ -2220,6 +2227,29 @@ __global__ void __launch_bounds__(256) k_select(Params p, Workspace ws, uint4 *_
     }
     dst[out_id] = make_uint4(bw[0], bw[1], bw[2], bw[3]);
     if (err_out) err_out[out_id] = best;
+}
+
+// Bounded exit: the probe stage's block (k_select over one mode with the
+// decode-aware choice, stored in ws.best_*) is final when its decode is within
+// p.bound_sse of the texels.  With the bound at the contract's absolute slack
+// (MSE 0.5 = SSE 32) such a block meets MSE <= MSE_ref * (1 + 1e-3) + 0.5
+// whatever the reference's own block is; every other block runs the full
+// search, so its output is the exact (or pruned) path's.
+__global__ void __launch_bounds__(256) k_bound(Params p, Workspace ws, uint4 *__restrict__ dst,
+                                               double *__restrict__ err_out)
+{
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= p.n) return;
+    const BlockMeta meta = ws.meta[b];
+    if (meta.flags & 5u) return;   // unsupported, or already final
+    const double e = ws.best_err[b];
+    if (!(e < 1.7976931348623157e308)) return;   // no candidate (the probed mode is not legal here)
+    const uint4 v = ws.best_blk[b];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    if (!(decoded_sse(w, ws.tex + (size_t)b * 64) <= p.bound_sse)) return;
+    dst[p.first + b] = v;
+    if (err_out) err_out[p.first + b] = e;
+    ws.meta[b].flags = meta.flags | 4u;
 }
 
 // ----------------------------------------------------------------- host ---
@@ -2649,6 +2679,8 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
         p.att = host_attempts(p, o.bc7_shake_ranks);
         p.decode_select = o.bc7_shake_ranks > 0 && !(p.err_thr > 0);
         p.dual_cap = 2 * (int)o.bc7_shake_ranks;
+        p.bound_sse = 0.0;
+        p.skip_done = 0;
         const uint32_t wg = 256;
         if (g)
             hipLaunchKernelGGL(k_prep_image, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, *g, p, ws);
@@ -2660,6 +2692,26 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
         const bool staged = p.err_thr > 0;
         const int order[8] = {6, 4, 3, 1, 2, 0, 7, 5};
         const uint32_t valid_modes = o.bc7_mode_mask == 0 ? 0xCFu : o.bc7_mode_mask;
+        if (o.bc7_mse_bound > 0.f && !staged) {
+            // bounded exit: probe modes 3 then 1 (visit positions 2 and 3; on
+            // G1 the cheapest modes to bring most blocks within the bound) with
+            // two partitions shaken; blocks within the bound drop out of every
+            // later launch (mode_active), the rest run the full search below.
+            Params pp = p;
+            pp.att = host_attempts(pp, 2);
+            pp.decode_select = 1;
+            pp.dual_cap = 4;
+            pp.bound_sse = 64.0 * (double)o.bc7_mse_bound;
+            for (int k = 2; k < 4; ++k) {
+                pp.stage_mask = 1u << order[k];
+                if (!(valid_modes & pp.stage_mask)) continue;
+                run_modes(pp, ws, st->sp, s);
+                hipLaunchKernelGGL(k_select, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, pp, ws, (uint4 *)dst, err,
+                                   k, k + 1, 0);
+                hipLaunchKernelGGL(k_bound, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, pp, ws, (uint4 *)dst, err);
+            }
+            p.skip_done = 1;
+        }
         int resume = 0;
         for (int k = 0; k < (staged ? 8 : 1); ++k) {
             p.stage_mask = staged ? (1u << order[k]) : 0xFFu;

@@ -74,6 +74,13 @@ typedef struct gic_options {
     uint8_t bc7enc_max_partitions;  /* mode-1 partitions scanned, 0..64 (default 64) */
     uint8_t bc7enc_least_squares;   /* m_try_least_squares (default 1) */
     uint8_t bc7enc_filterbank;      /* m_mode1_partition_estimation_filterbank (default 1) */
+    /* BC7 bounded exit (0 = off, the default): a cheap probe (modes 3 then 1,
+     * two partitions shaken) runs first and every block whose probe result
+     * DECODES within this per-block MSE (RGBA, 0..255 units, mean over the 64
+     * values) is final; only the other blocks run the full search.  With 0.5 --
+     * the absolute slack of the BC7 contract MSE <= MSE_ref * (1 + 1e-3) + 0.5 --
+     * every block meets the contract by construction. */
+    float bc7_mse_bound;
 } gic_options;
 
 void gic_default_options(gic_options *opt);

@@ -14,6 +14,12 @@ cores for it, far too long for a GPU test) and is committed as fixtures.
   of bit-identical blocks printed; and bit-identical to the oracle's model of
   the same pruned search on a live sub-sample.  (bc7_shake_ranks = 1 breaks
   the contract on the random sample: 27.7 MSE over on one block.)
+* bounded exit (bc7_mse_bound = 0.5, the contract's absolute slack): every
+  block either decodes within MSE 0.5 (a probe result, final by construction)
+  or is the full search's block -- bit-identical to the fixture under the
+  exact search -- and the whole sample meets the contract; on small images the
+  GPU equals a model of the probe built from oracle calls (mode 3, then mode 1,
+  two partitions shaken, then the exact search).
 """
 import json
 import os
@@ -68,13 +74,13 @@ def _device_image(name):
     return _src_cache[name]
 
 
-def _encode_rows(name, rows, shake_ranks):
+def _encode_rows(name, rows, shake_ranks, bound=0.0):
     """GPU blocks of the sample rows (None = every row), in fixture order."""
     import torch
     img, src = _device_image(name)
     h, w, _ = img.shape
     bx, by = (w + 3) // 4, (h + 3) // 4
-    opts = gic.Options(bc7_shake_ranks=shake_ranks)
+    opts = gic.Options(bc7_shake_ranks=shake_ranks, bc7_mse_bound=bound)
     if rows is None:
         dst = torch.zeros(bx * by * 16, dtype=torch.uint8, device="cuda")
         gic.encode_device(7, src, w, h, 1, 4, dst, opts)
@@ -131,3 +137,55 @@ def test_bc7_pruned_search_matches_its_oracle_model(gpu, shake_ranks):
         got = dst.cpu().numpy().reshape(-1, 16)
         ref = oracle_lib.encode_image_bc7(img, shake_ranks=shake_ranks)
         assert np.array_equal(got, ref), _mismatch_report(got, ref)
+
+
+@pytest.mark.parametrize("shake_ranks", [0, 2])
+@pytest.mark.parametrize("name,meta", _cases() or [pytest.param("missing", {}, marks=pytest.mark.skip)])
+def test_bc7_bounded_sample_8d(gpu, name, meta, shake_ranks):
+    rows = meta["rows"]
+    got = _encode_rows(name, rows, shake_ranks, bound=MSE_ABS)
+    ref = _fixture(name, got.shape[0])
+    src = _src_of(name, rows)
+    mg, mc = _block_mse(got, src), _block_mse(ref, src)
+    bad = np.nonzero(mg > mc * (1 + MSE_REL) + MSE_ABS)[0]
+    ident = (got == ref).all(axis=1)
+    probe = mg <= MSE_ABS
+    print(f"\n{name} bounded, shake_ranks={shake_ranks}: {got.shape[0]} blocks, {100 * ident.mean():.2f}% "
+          f"bit-identical, {100 * probe.mean():.2f}% within the bound, mean MSE {mg.mean():.4f} vs {mc.mean():.4f}")
+    assert len(bad) == 0, f"{len(bad)} blocks exceed the MSE tolerance, first {bad[:8].tolist()}"
+    if shake_ranks == 0:
+        other = np.nonzero(~(ident | probe))[0]
+        assert len(other) == 0, f"{len(other)} blocks neither final probes nor the exact block: {other[:8].tolist()}"
+
+
+def _mode_of(blocks):
+    b0 = blocks[:, 0].astype(np.int32)
+    return np.where(b0 == 0, -1, np.log2(np.maximum(b0 & -b0, 1)).astype(np.int32))
+
+
+def test_bc7_bounded_matches_model(gpu):
+    """The bounded path, block by block, is: the oracle's mode-3 search with 2
+    partitions shaken if that decodes within the bound, else its mode-1 search
+    likewise, else the exact search."""
+    import torch
+    g1 = synth.g1(8192, 8192)   # the bench texture: most blocks end in the probe
+    imgs = (np.ascontiguousarray(g1[4096:4112, 1024:1536]), np.ascontiguousarray(g1[:16, :256]),
+            synth.g1(128, 32, seed=5), _random_image()[120:136, :128])
+    for img in imgs:
+        h, w, _ = img.shape
+        src = torch.from_numpy(img[None].copy()).cuda()
+        nb = (w // 4) * (h // 4)
+        dst = torch.zeros(nb * 16, dtype=torch.uint8, device="cuda")
+        gic.encode_device(7, src, w, h, 1, 4, dst, gic.Options(bc7_mse_bound=MSE_ABS))
+        torch.cuda.synchronize()
+        got = dst.cpu().numpy().reshape(-1, 16)
+        sb = _src_blocks(img)
+        model = oracle_lib.encode_image_bc7(img)
+        done = np.zeros(nb, bool)
+        for mode in (3, 1):
+            cand = oracle_lib.encode_image_bc7(img, mode_mask=1 << mode, shake_ranks=2)
+            ok = ~done & (_mode_of(cand) == mode) & (_block_mse(cand, sb) <= MSE_ABS)
+            model[ok] = cand[ok]
+            done |= ok
+        print(f"\n{w}x{h}: {100 * done.mean():.1f}% of blocks final after the probe")
+        assert np.array_equal(got, model), _mismatch_report(got, model)
