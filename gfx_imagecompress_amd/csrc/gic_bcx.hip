@@ -140,78 +140,86 @@ __device__ __forceinline__ float ramp_fit_error(const Col &u, const float r[3][4
 }
 
 // Refine, amd_bcx_body.cpp:582-806 (R, then G, then B 3x3 jitter of both
-// endpoints on the 565 grid; RefinementSteps = `steps`)
+// endpoints on the 565 grid; RefinementSteps = `steps`).  One pass per
+// channel, a template on the channel so every index is static (a runtime
+// channel loop does not unroll and turns each array access into selects).
+template <int N, int CH, class Col>
+__device__ __forceinline__ void refine_pass(float cur[3][2], const float base[3][2], const Col &u, int lo, int hi,
+                                            float &best)
+{
+    const float wr = 0.3086f, wg = 0.6094f, wb = 0.0820f;
+    float wk[3][2], r[3][4], side[4][16];
+    {
+        const bool flat = expand_grid(wk, cur);
+        (void)flat;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) chan_ramp<N>(r[c], wk[c]);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            if (CH == CH_R) {
+                float dg = r[CH_G][k] - u.c(i, CH_G), db = r[CH_B][k] - u.c(i, CH_B);
+                side[k][i] = dg * dg * wg + db * db * wb;
+            } else if (CH == CH_G) {
+                float dr = r[CH_R][k] - u.c(i, CH_R), db = r[CH_B][k] - u.c(i, CH_B);
+                side[k][i] = dr * dr * wr + db * db * wb;
+            } else {
+                float dr = r[CH_R][k] - u.c(i, CH_R), dg = r[CH_G][k] - u.c(i, CH_G);
+                side[k][i] = dr * dr * wr + dg * dg * wg;
+            }
+        }
+    const float grid = (float)(1 << (8 - chan_bits(CH)));
+    const float wc = (CH == CH_R) ? wr : (CH == CH_G) ? wg : wb;
+    float b0 = base[CH][0], b1 = base[CH][1];
+    for (int a = lo; a <= hi; ++a)
+        for (int b = lo; b <= hi; ++b) {
+            cur[CH][0] = minr(maxr(base[CH][0] + (float)a * grid, 0.f), 255.f);
+            cur[CH][1] = minr(maxr(base[CH][1] + (float)b * grid, 0.f), 255.f);
+            const bool flat = expand_grid(wk, cur);
+            chan_ramp<N>(r[CH], wk[CH]);
+            float mse = 0.f;
+            const int nr = flat ? 1 : N;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                float m = 10000000.f;
+#pragma unroll
+                for (int k = 0; k < N; ++k) {
+                    float d = r[CH][k] - u.c(i, CH);
+                    float e = side[k][i] + d * d * wc;
+                    m = (k < nr) ? minr(m, e) : m;
+                }
+                mse += m * u.rpt(i);   // count 0 past n: adds +0
+            }
+            if (mse < best) {
+                b0 = cur[CH][0];
+                b1 = cur[CH][1];
+                best = mse;
+            }
+        }
+    cur[CH][0] = b0;
+    cur[CH][1] = b1;
+}
+
 template <int N, class Col>
 __device__ __forceinline__ void refine_channels(float cur[3][2], const Col &u, int steps)
 {
-    const float wr = 0.3086f, wg = 0.6094f, wb = 0.0820f;
     float base[3][2], wk[3][2], r[3][4];
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
         base[ch][0] = cur[ch][0];
         base[ch][1] = cur[ch][1];
     }
-    bool flat = expand_grid(wk, cur);
+    const bool flat = expand_grid(wk, cur);
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) chan_ramp<N>(r[ch], wk[ch]);
     float best = ramp_fit_error<N>(u, r, flat);
     if (best == 0.f || !steps) return;
     const int lo = -(int)minr((float)steps, 8.f), hi = (int)minr((float)steps, 8.f);
-    float side[4][16];
-#pragma unroll
-    for (int pass = 0; pass < 3; ++pass) {
-        const int ch = pass == 0 ? CH_R : pass == 1 ? CH_G : CH_B;
-        if (pass > 0) {
-            flat = expand_grid(wk, cur);
-#pragma unroll
-            for (int c = 0; c < 3; ++c) chan_ramp<N>(r[c], wk[c]);
-        }
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-#pragma unroll
-            for (int k = 0; k < N; ++k) {
-                if (ch == CH_R) {
-                    float dg = r[CH_G][k] - u.c(i, CH_G), db = r[CH_B][k] - u.c(i, CH_B);
-                    side[k][i] = dg * dg * wg + db * db * wb;
-                } else if (ch == CH_G) {
-                    float dr = r[CH_R][k] - u.c(i, CH_R), db = r[CH_B][k] - u.c(i, CH_B);
-                    side[k][i] = dr * dr * wr + db * db * wb;
-                } else {
-                    float dr = r[CH_R][k] - u.c(i, CH_R), dg = r[CH_G][k] - u.c(i, CH_G);
-                    side[k][i] = dr * dr * wr + dg * dg * wg;
-                }
-            }
-        const float grid = (float)(1 << (8 - chan_bits(ch)));
-        const float wc = (ch == CH_R) ? wr : (ch == CH_G) ? wg : wb;
-        float b0 = base[ch][0], b1 = base[ch][1];
-        for (int a = lo; a <= hi; ++a)
-            for (int b = lo; b <= hi; ++b) {
-                cur[ch][0] = minr(maxr(base[ch][0] + (float)a * grid, 0.f), 255.f);
-                cur[ch][1] = minr(maxr(base[ch][1] + (float)b * grid, 0.f), 255.f);
-                flat = expand_grid(wk, cur);
-                chan_ramp<N>(r[ch], wk[ch]);
-                float mse = 0.f;
-                const int nr = flat ? 1 : N;
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    float m = 10000000.f;
-#pragma unroll
-                    for (int k = 0; k < N; ++k) {
-                        float d = r[ch][k] - u.c(i, ch);
-                        float e = side[k][i] + d * d * wc;
-                        m = (k < nr) ? minr(m, e) : m;
-                    }
-                    mse += m * u.rpt(i);   // count 0 past n: adds +0
-                }
-                if (mse < best) {
-                    b0 = cur[ch][0];
-                    b1 = cur[ch][1];
-                    best = mse;
-                }
-            }
-        cur[ch][0] = b0;
-        cur[ch][1] = b1;
-    }
+    refine_pass<N, CH_R>(cur, base, u, lo, hi, best);
+    refine_pass<N, CH_G>(cur, base, u, lo, hi, best);
+    refine_pass<N, CH_B>(cur, base, u, lo, hi, best);
 }
 
 // Refine3D, amd_bcx_body.cpp:808-932 (b3DRefinement): the joint jitter of all
@@ -705,17 +713,46 @@ struct TexB {
     uint32_t thr_final;   // smallest alpha byte a with (float)a >= thr01 * 255.f
     __device__ __forceinline__ float ch(int i, int c) const { return (float)((px[i] >> (8 * c)) & 255u); }
     __device__ __forceinline__ bool transparent(int i) const { return (px[i] >> 24) < thr_final; }
+    __device__ __forceinline__ const TexB &view() const { return *this; }
 };
 struct TexF {
     const float *in;
     float thr;   // thr01 * 255.f
     __device__ __forceinline__ float ch(int i, int c) const { return in[i * 4 + c] * 255.0f; }
     __device__ __forceinline__ bool transparent(int i) const { return !(in[i * 4 + 3] * 255.0f >= thr); }
+    __device__ __forceinline__ const TexF &view() const { return *this; }
+};
+// The block's texels by value (TexG::view)
+struct TexV {
+    uint32_t px[16];
+    uint32_t thr_final;
+    __device__ __forceinline__ float ch(int i, int c) const { return (float)((px[i] >> (8 * c)) & 255u); }
+    __device__ __forceinline__ bool transparent(int i) const { return (px[i] >> 24) < thr_final; }
+};
+// Texels re-read from the image when the final clustering needs them: the 16
+// words are not held in VGPRs through the endpoint search (L2 hits; the
+// source address is made opaque so the compiler cannot reuse the first load).
+struct TexG {
+    Geometry g;
+    uint32_t slice, by, bx;
+    bool force_alpha_one;
+    uint32_t thr_final;
+    __device__ __forceinline__ TexV view() const
+    {
+        Geometry gg = g;
+        const uint8_t *src = gg.src;
+        asm volatile("" : "+s"(src));
+        gg.src = src;
+        TexV v;
+        v.thr_final = thr_final;
+        load_block_u8(gg, slice, by, bx, force_alpha_one, v.px);
+        return v;
+    }
 };
 
 // Clstr -> ClstrBas -> ClstrIntnl, amd_bcx_body.cpp:258-378
 template <int N, class Tex>
-__device__ __forceinline__ uint32_t final_indices(const Tex &t, const uint8_t ep[3][2], bool use_alpha, float &err)
+__device__ __forceinline__ uint32_t final_indices(const Tex &tex, const uint8_t ep[3][2], bool use_alpha, float &err)
 {
     const float w0 = 0.3086f, w1 = 0.6094f, w2 = 0.0820f;
     const unsigned c0 = ((unsigned)(ep[CH_R][0] & 0xf8) << 8) | ((unsigned)(ep[CH_G][0] & 0xfc) << 3) |
@@ -735,6 +772,7 @@ __device__ __forceinline__ uint32_t final_indices(const Tex &t, const uint8_t ep
     const int nr = flat ? 1 : N;
     uint32_t bits = 0;
     err = 0.f;
+    const auto &t = tex.view();
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const float R = t.ch(i, 0), G = t.ch(i, 1), B = t.ch(i, 2);
@@ -825,13 +863,12 @@ __device__ __forceinline__ uint2 encode_bc1(const Col &u, int kept, const Tex &t
 
 template <bool R3D>
 __device__ __forceinline__ uint2 encode_bc1_u8(const uint32_t px[16], int steps, bool use_alpha, uint32_t thr_keep,
-                                               uint32_t thr_final, const volatile float *lut)
+                                               const TexG &t, const volatile float *lut)
 {
     ColB u;
     u.lut = lut;
     int kept;
     unique_colours(u, px, use_alpha, thr_keep, kept);
-    const TexB t{px, thr_final};
     return encode_bc1<R3D>(u, kept, t, steps, use_alpha);
 }
 
@@ -1136,7 +1173,7 @@ struct Bc1Params {
 };
 
 template <bool R3D>
-__global__ void __launch_bounds__(256, 2) bc1_image_kernel(Geometry g, Bc1Params p, uint2 *__restrict__ dst)
+__global__ void __launch_bounds__(256, R3D ? 2 : 3) bc1_image_kernel(Geometry g, Bc1Params p, uint2 *__restrict__ dst)
 {
     __shared__ float lut[256];   // byte -> v / 255.0f
     lut[threadIdx.x] = (float)threadIdx.x / 255.0f;
@@ -1147,7 +1184,8 @@ __global__ void __launch_bounds__(256, 2) bc1_image_kernel(Geometry g, Bc1Params
     block_coords(g, id, slice, by, bx);
     uint32_t px[16];
     load_block_u8(g, slice, by, bx, p.force_alpha_one != 0, px);
-    dst[id] = bcx::encode_bc1_u8<R3D>(px, p.steps, p.alpha_threshold > 0.0f, p.thr_keep, p.thr_final, lut);
+    const bcx::TexG t{g, slice, by, bx, p.force_alpha_one != 0, p.thr_final};
+    dst[id] = bcx::encode_bc1_u8<R3D>(px, p.steps, p.alpha_threshold > 0.0f, p.thr_keep, t, lut);
 }
 
 // BC2 / BC3 (amd_bc2_compressor.cpp:36-50, amd_bc3_compressor.cpp:36-50): alpha
