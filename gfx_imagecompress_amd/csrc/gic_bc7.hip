@@ -2567,14 +2567,19 @@ static hipError_t get_state(uint32_t chunk, int nsets, DeviceState *&out)
 }
 
 // K1-K3 for the modes of p.stage_mask (kernels return early for inactive work)
-static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, hipStream_t s)
+// `integral`: every block of the chunk has integral texels in [0, 255] (an
+// 8-bit image source: v / 255.0f * 255.0f is exact for every byte), so the
+// f64 fallback kernels (k_quant, k_shake, k_dual_quant, k_dual) would only
+// read the flags and exit; they are not launched (their 1-wave/SIMD grids
+// otherwise wait for whole SIMDs behind the other lane's shakers).
+static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, hipStream_t s, bool integral)
 {
     const uint32_t wg = 256;
     const uint32_t sm = p.stage_mask;
     const bool single = (sm & 0xCFu) != 0, dual = (sm & 0x30u) != 0;
     if (single) {
         const uint64_t nq = (uint64_t)p.n * kQuantTasks;
-        hipLaunchKernelGGL(k_quant, dim3((uint32_t)((nq + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
+        if (!integral) hipLaunchKernelGGL(k_quant, dim3((uint32_t)((nq + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
         const uint64_t nq3 = (uint64_t)p.n * 208, nq4 = (uint64_t)p.n * 65;
         if (sm & 0x0Fu) {
             const uint64_t nu = (uint64_t)p.n * g_nu;
@@ -2588,7 +2593,7 @@ static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, h
             hipLaunchKernelGGL(k_quant_trace, dim3((uint32_t)((nt + 63) / 64)), dim3(64), 0, s, p, ws);
         }
         const uint64_t ns = (uint64_t)p.n * kShakeSlots * kShakeRanks;
-        hipLaunchKernelGGL(k_shake, dim3((uint32_t)((ns + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
+        if (!integral) hipLaunchKernelGGL(k_shake, dim3((uint32_t)((ns + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
         if ((sm & 0x03u) && wave_count<8>(p.att)) {
             const uint64_t nw8 = (uint64_t)p.n * wave_count<8>(p.att) * 64;
             hipLaunchKernelGGL(k_shake_wave<8>, dim3((uint32_t)((nw8 + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
@@ -2604,12 +2609,12 @@ static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, h
     }
     if (dual) {
         const uint64_t ndq = (uint64_t)p.n * kDualTasks * 2;
-        hipLaunchKernelGGL(k_dual_quant, dim3((uint32_t)((ndq + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
+        if (!integral) hipLaunchKernelGGL(k_dual_quant, dim3((uint32_t)((ndq + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
         hipLaunchKernelGGL(k_dual_quant_reg, dim3((uint32_t)((ndq + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
         if (p.quant_thr < 255.0)
             hipLaunchKernelGGL(k_dual_quant_trace, dim3((uint32_t)((ndq + 63) / 64)), dim3(64), 0, s, p, ws);
         const uint64_t nd = (uint64_t)p.n * kDualTasks;
-        hipLaunchKernelGGL(k_dual, dim3((uint32_t)((nd + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
+        if (!integral) hipLaunchKernelGGL(k_dual, dim3((uint32_t)((nd + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
         const uint64_t ndw = (uint64_t)p.n * kDualTasks * 2 * 64;
         hipLaunchKernelGGL(k_dual_wave, dim3((uint32_t)((ndw + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
     }
@@ -2705,7 +2710,7 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
             for (int k = 2; k < 4; ++k) {
                 pp.stage_mask = 1u << order[k];
                 if (!(valid_modes & pp.stage_mask)) continue;
-                run_modes(pp, ws, st->sp, s);
+                run_modes(pp, ws, st->sp, s, g != nullptr);
                 hipLaunchKernelGGL(k_select, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, pp, ws, (uint4 *)dst, err,
                                    k, k + 1, 0);
                 hipLaunchKernelGGL(k_bound, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, pp, ws, (uint4 *)dst, err);
@@ -2718,7 +2723,7 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
             const bool last = !staged || k == 7;
             const bool skip = staged && !(valid_modes & p.stage_mask);
             if (skip && !last) continue;
-            if (!skip) run_modes(p, ws, st->sp, s);
+            if (!skip) run_modes(p, ws, st->sp, s, g != nullptr);
             hipLaunchKernelGGL(k_select, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, p, ws, (uint4 *)dst, err,
                                staged ? k : 0, staged ? k + 1 : 8, resume);
             resume = 1;
