@@ -740,8 +740,15 @@ __device__ __forceinline__ void est_setup(EstSubset &e)
     }
 }
 
+//
+// `best` is the least total so far: once every lane of the wave has a partial
+// sum at or above its own best, the rest cannot make the shape win (the terms
+// are non-negative and the caller keeps a total only if it is strictly less),
+// so the sum stops -- the reference's own early exit (:1156-1157), taken per
+// wave after every four texels.
 template <bool P>
-__device__ __forceinline__ uint32_t estimate2(uint32_t m0, const uint32_t px[16], const Ycc &tx, const EncCfg &cf)
+__device__ __forceinline__ uint32_t estimate2(uint32_t m0, const uint32_t px[16], const Ycc &tx, const EncCfg &cf,
+                                              uint32_t best)
 {
     EstSubset s0, s1;
 #pragma unroll
@@ -763,6 +770,7 @@ __device__ __forceinline__ uint32_t estimate2(uint32_t m0, const uint32_t px[16]
     uint32_t tot = 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
+        if ((i & 3) == 0 && i > 0 && __all(tot >= best)) break;
         const bool in0 = (m0 >> i) & 1u;
         int lo[3], hi[3], th[7];
         int d = 0;
@@ -817,7 +825,7 @@ __device__ __forceinline__ uint32_t pick_partition(const uint32_t px[16], const 
             continue;
         }
         const uint32_t m0 = shape_mask(kBc7Shape2[part], 0);
-        const uint32_t e = estimate2<P>(m0, px, tx, cf);
+        const uint32_t e = estimate2<P>(m0, px, tx, cf, best);
         if (e < best) best = e, best_part = part;
         if (part == 34 && best_part != 34) stop = true;
         if (it == 13) key = best_part;
