@@ -745,7 +745,7 @@ __device__ __forceinline__ void est_setup(EstSubset &e)
 // sum at or above its own best, the rest cannot make the shape win (the terms
 // are non-negative and the caller keeps a total only if it is strictly less),
 // so the sum stops -- the reference's own early exit (:1156-1157), taken per
-// wave after every four texels.
+// wave after every two texels.
 template <bool P>
 __device__ __forceinline__ uint32_t estimate2(uint32_t m0, const uint32_t px[16], const Ycc &tx, const EncCfg &cf,
                                               uint32_t best)
@@ -770,7 +770,7 @@ __device__ __forceinline__ uint32_t estimate2(uint32_t m0, const uint32_t px[16]
     uint32_t tot = 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        if ((i & 3) == 0 && i > 0 && __all(tot >= best)) break;
+        if ((i & 1) == 0 && i > 0 && __all(tot >= best)) break;
         const bool in0 = (m0 >> i) & 1u;
         int lo[3], hi[3], th[7];
         int d = 0;
