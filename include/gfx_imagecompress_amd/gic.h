@@ -79,7 +79,8 @@ typedef struct gic_options {
      * DECODES within this per-block MSE (RGBA, 0..255 units, mean over the 64
      * values) is final; only the other blocks run the full search.  With 0.5 --
      * the absolute slack of the BC7 contract MSE <= MSE_ref * (1 + 1e-3) + 0.5 --
-     * every block meets the contract by construction. */
+     * every block meets the contract by construction.  Ignored below
+     * quality 0.25, where the reference's own error-threshold exit is in force. */
     float bc7_mse_bound;
 } gic_options;
 
