@@ -67,6 +67,9 @@ def test_block_bytes_and_argument_checks():
     assert lib.gic_hip_encode(gic.FMT_BC7ENC16, 16, 4, 4, 1, 4, 16, ctypes.byref(o), 16, None, None) == gic.GIC_EINVAL
     assert lib.gic_hip_encode_blocks_u8(gic.FMT_BC7, 16, 1, None, 16, None) == gic.GIC_EINVAL
     assert lib.gic_hip_encode_blocks_u8(gic.FMT_BC7ENC16, None, 1, None, 16, None) == gic.GIC_EINVAL
+    for bound in (float("nan"), -1.0, 70000.0):   # bc7_mse_bound: NaN, negative, above 255^2
+        o = gic.Options(bc7_mse_bound=bound).to_c()
+        assert lib.gic_hip_encode(gic.FMT_BC7, 16, 4, 4, 1, 4, 16, ctypes.byref(o), 16, None, None) == gic.GIC_EINVAL
 
 
 def test_image_model_and_pick_type():
