@@ -59,6 +59,9 @@ def lib() -> ctypes.CDLL:
         _lib.orc_bc7_block.argtypes = [vp, ctypes.c_uint8, ctypes.c_int, ctypes.c_float, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_float, vp]
         _lib.orc_bc7_block.restype = ctypes.c_double
+        _lib.orc_bc7_block_ex.argtypes = [vp, ctypes.c_uint8, ctypes.c_int, ctypes.c_float, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_float, ctypes.c_int, vp]
+        _lib.orc_bc7_block_ex.restype = ctypes.c_double
         _lib.orc_fnv1a64.argtypes = [vp, ctypes.c_size_t]
         _lib.orc_fnv1a64.restype = ctypes.c_uint64
         _lib.orc_bc7_shake_ramp.argtypes = [ctypes.c_int] * 5
@@ -166,6 +169,20 @@ def bc7_block(block: np.ndarray, mode_mask: int = 0xFF):
     out = np.zeros(16, np.uint8)
     e = lib().orc_bc7_block(b.ctypes.data, mode_mask, 1, 1.0, 1, 1, 1.0, out.ctypes.data)
     return out.tobytes(), e
+
+
+def bc7_blocks_ex(blocks: np.ndarray, mode_mask: int = 0xFF, colour_restrict: bool = True, shake_ranks: int = 0,
+                  has_alpha: bool = True) -> np.ndarray:
+    """orc_bc7_block_ex over (n, 16, 4) uint8 blocks (texels as v / 255.0f, the
+    image driver's conversion), with the encoder's colour restriction and the
+    GPU's shake-rank cap selectable."""
+    b = np.ascontiguousarray(blocks, dtype=np.uint8).reshape(-1, 64)
+    out = np.zeros((b.shape[0], 16), np.uint8)
+    for k in range(b.shape[0]):
+        f = (b[k].astype(np.float32) / np.float32(255.0)).astype(np.float32)
+        lib().orc_bc7_block_ex(f.ctypes.data, mode_mask, int(has_alpha), 1.0, int(colour_restrict), 1, 1.0,
+                               shake_ranks, out[k].ctypes.data)
+    return out
 
 
 def encode_image_bc7enc(img: np.ndarray, fast: bool = False, perceptual: bool = True) -> np.ndarray:

@@ -18,8 +18,9 @@ cores for it, far too long for a GPU test) and is committed as fixtures.
   block either decodes within MSE 0.5 (a probe result, final by construction)
   or is the full search's block -- bit-identical to the fixture under the
   exact search -- and the whole sample meets the contract; on small images the
-  GPU equals a model of the probe built from oracle calls (mode 3, then mode 1,
-  two partitions shaken, then the exact search).
+  GPU equals a model of the probe built from oracle calls (mode 6 without the
+  colour restriction, mode 3, then mode 1, two partitions shaken, then the exact
+  search).
 """
 import json
 import os
@@ -164,12 +165,13 @@ def _mode_of(blocks):
 
 
 def test_bc7_bounded_matches_model(gpu):
-    """The bounded path, block by block, is: the oracle's mode-3 search with 2
-    partitions shaken if that decodes within the bound, else its mode-1 search
-    likewise, else the exact search."""
+    """The bounded path, block by block, is: the oracle's mode-6 search (no
+    colour restriction) with 2 partitions shaken if that decodes within the
+    bound, else its mode-3 search likewise, else mode 1, else the exact search."""
     import torch
     g1 = synth.g1(8192, 8192)   # the bench texture: most blocks end in the probe
-    imgs = (np.ascontiguousarray(g1[4096:4112, 1024:1536]), np.ascontiguousarray(g1[:16, :256]),
+    mixed = np.ascontiguousarray(np.concatenate([g1[2048:2064, 512:640], synth.g1(128, 16, seed=5)], axis=1))
+    imgs = (np.ascontiguousarray(g1[4096:4112, 1024:1536]), np.ascontiguousarray(g1[:16, :256]), mixed,
             synth.g1(128, 32, seed=5), _random_image()[120:136, :128])
     for img in imgs:
         h, w, _ = img.shape
@@ -182,8 +184,8 @@ def test_bc7_bounded_matches_model(gpu):
         sb = _src_blocks(img)
         model = oracle_lib.encode_image_bc7(img)
         done = np.zeros(nb, bool)
-        for mode in (3, 1):
-            cand = oracle_lib.encode_image_bc7(img, mode_mask=1 << mode, shake_ranks=2)
+        for mode in (6, 3, 1):
+            cand = oracle_lib.bc7_blocks_ex(sb, mode_mask=1 << mode, colour_restrict=False, shake_ranks=2)
             ok = ~done & (_mode_of(cand) == mode) & (_block_mse(cand, sb) <= MSE_ABS)
             model[ok] = cand[ok]
             done |= ok

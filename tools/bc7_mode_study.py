@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--rows", type=int, default=256)
     ap.add_argument("--size", type=int, default=8192)
     ap.add_argument("--shake-ranks", type=int, default=0)
+    ap.add_argument("--no-colour-restrict", action="store_true", help="let opaque blocks use modes 4-7")
     ap.add_argument("--masks", default="", help="comma-separated hex mode masks (default: ff and each mode)")
     ap.add_argument("--out", default="gpurun_out/mode_study.npz")
     a = ap.parse_args()
@@ -39,7 +40,7 @@ def main():
     s = torch.cuda.current_stream()
     masks = [int(x, 16) for x in a.masks.split(",")] if a.masks else [0xFF] + [1 << m for m in range(8)]
     for mask in masks:
-        o = gic.Options(bc7_mode_mask=mask, bc7_shake_ranks=a.shake_ranks)
+        o = gic.Options(bc7_mode_mask=mask, bc7_shake_ranks=a.shake_ranks, colour_restrict=not a.no_colour_restrict)
         gic.encode_device(gic.FMT_BC7, src, size, rows * 4, 1, 4, dst, o)   # warm (tables, workspaces)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
