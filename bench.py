@@ -227,7 +227,7 @@ def bc7_secondary(args, gic, src, size, avail_rows, world, dev, rank, shake_rank
     search = "exact (reference search, bit-identical)" if shake_ranks == 0 else \
         f"pruned: {shake_ranks} partitions shaken per mode (per-block MSE tolerance)"
     if bound > 0:
-        search = (f"bounded exit: blocks whose mode-3/mode-1 probe decodes within MSE {bound:g} are final "
+        search = (f"bounded exit: blocks whose mode-6/3/1 probe decodes within MSE {bound:g} are final "
                   f"(contract met by construction), the rest " +
                   ("the exact search" if shake_ranks == 0 else f"the pruned search ({shake_ranks} partitions)"))
     res = {"metric": f"Mpixels/s BC7 quality {args.bc7_quality:g} (all modes, shakers on), {search}",

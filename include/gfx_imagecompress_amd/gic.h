@@ -74,7 +74,7 @@ typedef struct gic_options {
     uint8_t bc7enc_max_partitions;  /* mode-1 partitions scanned, 0..64 (default 64) */
     uint8_t bc7enc_least_squares;   /* m_try_least_squares (default 1) */
     uint8_t bc7enc_filterbank;      /* m_mode1_partition_estimation_filterbank (default 1) */
-    /* BC7 bounded exit (0 = off, the default): a cheap probe (modes 3 then 1,
+    /* BC7 bounded exit (0 = off, the default): a cheap probe (modes 6, 3, then 1, mode 6 also on opaque blocks,
      * two partitions shaken) runs first and every block whose probe result
      * DECODES within this per-block MSE (RGBA, 0..255 units, mean over the 64
      * values) is final; only the other blocks run the full search.  With 0.5 --
