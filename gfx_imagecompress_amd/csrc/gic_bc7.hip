@@ -2590,8 +2590,11 @@ static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, h
             hipLaunchKernelGGL(k_quant_sub, dim3((uint32_t)((nu + wg - 1) / wg)), dim3(wg), 0, s, p, ws, g_nu);
             hipLaunchKernelGGL(k_quant_gather, dim3((uint32_t)((nq3 + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
         }
-        if (sm & 0xC0u)
+        if ((sm & 0xC0u) == 0x40u) {   // mode 6 alone (the bounded-exit probe): one lane per block
+            hipLaunchKernelGGL(k_quant_reg<4>, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, p, ws, 208, 1);
+        } else if (sm & 0xC0u) {
             hipLaunchKernelGGL(k_quant_reg<4>, dim3((uint32_t)((nq4 + wg - 1) / wg)), dim3(wg), 0, s, p, ws, 208, 65);
+        }
         if (p.quant_thr < 255.0 && (sm & 0x8Fu)) {
             const uint64_t nt = (uint64_t)p.n * 272;
             hipLaunchKernelGGL(k_quant_trace, dim3((uint32_t)((nt + 63) / 64)), dim3(64), 0, s, p, ws);
