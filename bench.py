@@ -68,7 +68,8 @@ def parse():
                         "texture (-1 = the whole 8K texture, 0 = skip)")
     p.add_argument("--no-bc45", action="store_true", help="skip the BC4/BC5 8K legs (configs[2])")
     p.add_argument("--bc7-mse-bound", type=float, default=0.5,
-                   help="BC7 bounded-exit legs: per-block MSE under which the probe's block is final (0 = no legs)")
+                   help="BC7 bounded-exit legs: per-block MSE under which the probe's block is final (0 = no legs); "
+                        "the batch64 workload uses this value too (0 = no exit)")
     p.add_argument("--no-bc7enc", action="store_true", help="skip the bc7enc16 (fast BC7 path) legs")
     p.add_argument("--bc7-shake-ranks", type=int, default=2,
                    help="pruned BC7 search leg: partitions shaken per single-index mode (gic_options."
@@ -431,7 +432,8 @@ def batch_workload(args, gic, world, rank, dev):
     first, rows = shard.shard_rows(by, world, rank)
     src = synth.g1_torch(n, n, S, seed=0x9E3779B9, device=dev)
     dst = torch.empty(max(1, S * rows * bx * 16), dtype=torch.uint8, device=dev)
-    opts = gic.Options(bc7_quality=args.bc7_quality, bc7_shake_ranks=args.bc7_shake_ranks)
+    opts = gic.Options(bc7_quality=args.bc7_quality, bc7_shake_ranks=args.bc7_shake_ranks,
+                       bc7_mse_bound=args.bc7_mse_bound)
     stream = torch.cuda.current_stream(dev)
     # warm-up: the per-device tables and workspaces (one block row of one slice)
     gic.encode_device(7, src[:1], n, n, 1, 4, dst, opts, first, 1, stream=stream)
@@ -477,8 +479,11 @@ def batch_workload(args, gic, world, rank, dev):
                                    f"{'RCCL' if world == 1 or dist.get_backend() != 'gloo' else 'gloo (rehearsal)'} "
                                    f"all-gather to rank 0 timed separately",
                        "format": "BC7", "slices": S, "width": n, "global_batch_blocks": total_blocks,
-                       "bc7_search": "exact" if args.bc7_shake_ranks == 0 else
-                       f"pruned, {args.bc7_shake_ranks} partitions shaken per mode (per-block MSE tolerance)",
+                       "bc7_search": ("exact" if args.bc7_shake_ranks == 0 else
+                                      f"pruned, {args.bc7_shake_ranks} partitions shaken per mode "
+                                      f"(per-block MSE tolerance)") +
+                                     (f"; bounded exit: blocks whose mode-6/3/1 probe decodes within MSE "
+                                      f"{args.bc7_mse_bound:g} are final" if args.bc7_mse_bound > 0 else ""),
                        "parallelism": f"block-row shards x{world}",
                        "world_size_seen": dist.get_world_size() if world > 1 else 1},
             "blocks_per_s": round(total_blocks * args.steps / wall, 1),
@@ -502,16 +507,29 @@ def batch_workload(args, gic, world, rank, dev):
             ref = oracle_lib.encode_image_bc7(img, quality=args.bc7_quality, first_row=row, num_rows=1,
                                               threads=threads)
             dt = time.perf_counter() - c0   # the reference search: the CPU baseline
+            got = host_rows[sl, row]
+            if args.bc7_mse_bound > 0:
+                # bounded exit: the per-block MSE contract against the exact search
+                t = img[4 * row:4 * row + 4, :bx * 4].reshape(4, bx, 4, 4).transpose(1, 0, 2, 3)
+                t = t.reshape(bx, 16, 4).astype(np.float64)
+                mg = ((oracle_lib.bc7_decode(got).astype(np.float64) - t) ** 2).mean(axis=(1, 2))
+                mc = ((oracle_lib.bc7_decode(ref).astype(np.float64) - t) ** 2).mean(axis=(1, 2))
+                contract = (f"; {int((mg > mc * 1.001 + 0.5).sum())} blocks outside the MSE contract vs the "
+                            f"exact search, mean MSE {mg.mean():.4f} vs {mc.mean():.4f}, "
+                            f"{int((mg <= args.bc7_mse_bound).sum())}/{bx} within the exit bound")
+            else:
+                contract = ""
             if args.bc7_shake_ranks:
                 ref = oracle_lib.encode_image_bc7(img, quality=args.bc7_quality, first_row=row, num_rows=1,
                                                   threads=threads, shake_ranks=args.bc7_shake_ranks)
-            same = int((host_rows[sl, row] == ref).all(axis=1).sum())
+            same = int((got == ref).all(axis=1).sum())
             line["cpu_baseline"] = {"value": round(4 * n / dt / 1e6, 6), "unit": "Mpixels/s", "cores": threads,
                                     "kind": "port", "cpu_model": cpu_model(),
                                     "sample": f"slice {sl} block row {row} ({bx} blocks, {dt:.1f} s)",
                                     "blocks_per_s": round(bx / dt, 1)}
             line["gpu_parity"] = (f"{same}/{bx} blocks of slice {sl} row {row} (after the gather) bit-identical "
-                                  f"to the oracle running the same search")
+                                  f"to the oracle running the same search" +
+                                  (" without the exit" if args.bc7_mse_bound > 0 else "") + contract)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
