@@ -13,8 +13,9 @@ configs[3] leg (BC7 default quality over the same texture, one pass) and
 configs[2] legs (BC4 R8 height map, BC5 RG8 normal map, 8192^2).
 
 --workload batch64 = configs[4]: BC7 over a fixed 64 x 4096^2 G1 stack, every
-slice's block rows split over the N ranks (strong scaling), one timed RCCL
-all-gather of the packed bitstream at the end.
+slice's block rows split over the N ranks (strong scaling; chunks of
+--shard-chunk block rows dealt round-robin), one timed RCCL gather of the
+packed bitstream to rank 0 at the end.
 
 --gpus N without torchrun's environment starts N ranks itself (a
 torch.distributed.run child process, before any GPU call); under torchrun
@@ -71,17 +72,24 @@ def parse():
                    help="BC7 bounded-exit legs: per-block MSE under which the probe's block is final (0 = no legs); "
                         "the batch64 workload uses this value too (0 = no exit)")
     p.add_argument("--no-bc7enc", action="store_true", help="skip the bc7enc16 (fast BC7 path) legs")
-    p.add_argument("--bc7-shake-ranks", type=int, default=2,
-                   help="pruned BC7 search leg: partitions shaken per single-index mode (gic_options."
-                        "bc7_shake_ranks; 0 = skip the pruned leg).  The exact search (the reference's 8) is "
-                        "always timed; the batch64 workload uses this value (0 = exact)")
+    p.add_argument("--bc7-shake-ranks", type=int, default=None,
+                   help="pruned BC7 search: partitions shaken per single-index mode (gic_options."
+                        "bc7_shake_ranks).  8k workload: the pruned legs (default 2; 0 = skip them; the exact "
+                        "search is always timed).  batch64: the survivors' search (default 0 = exact, so with "
+                        "the bounded exit every block meets the MSE contract by construction)")
     p.add_argument("--workload", default="8k", choices=["8k", "batch64"],
                    help="8k: configs[1] (+ configs[2]/[3] legs); batch64: configs[4], BC7 over a fixed stack "
                         "of --batch-slices x --batch-size^2 G1 slices, block rows of every slice split over "
                         "the ranks (strong scaling) and one timed RCCL gather to rank 0")
     p.add_argument("--batch-slices", type=int, default=64)
     p.add_argument("--batch-size", type=int, default=4096)
-    return p.parse_args()
+    p.add_argument("--shard-chunk", type=int, default=16,
+                   help="batch64: block rows per chunk dealt round-robin over the ranks (0 = one contiguous "
+                        "range per rank)")
+    a = p.parse_args()
+    if a.bc7_shake_ranks is None:
+        a.bc7_shake_ranks = 0 if a.workload == "batch64" else 2
+    return a
 
 
 def cpu_model():
@@ -183,17 +191,31 @@ def _max_over_ranks(t, world):
     return t
 
 
-def _gather_all(dst, world):
-    """All-gather of every rank's packed blocks into one buffer."""
+def _gather_root(dst, world):
+    """One gather of every rank's (equal-size) packed blocks to rank 0 (RCCL
+    on device tensors, gloo on host ones); the concatenation on rank 0, None
+    elsewhere."""
     import torch
     import torch.distributed as dist
-    if dist.get_backend() == "gloo":
-        parts = [torch.empty_like(dst, device="cpu") for _ in range(world)]
-        dist.all_gather(parts, dst.cpu())
-        return torch.cat(parts)
-    out_all = torch.empty(world * dst.numel(), dtype=torch.uint8, device=dst.device)
-    dist.all_gather_into_tensor(out_all, dst)
-    return out_all
+    gloo = dist.get_backend() == "gloo"
+    loc = dst.cpu() if gloo else dst
+    parts = [torch.empty_like(loc) for _ in range(world)] if dist.get_rank() == 0 else None
+    dist.gather(loc, gather_list=parts, dst=0)
+    return torch.cat(parts) if parts is not None else None
+
+
+def _spread_over_ranks(v, world):
+    """[min, max] over ranks of one float (per-rank kernel time: the load
+    balance of the shards)."""
+    import torch
+    import torch.distributed as dist
+    if world <= 1:
+        return [float(v), float(v)]
+    gloo = dist.get_backend() == "gloo"
+    dev = "cpu" if gloo else torch.device("cuda", torch.cuda.current_device())
+    t = torch.tensor([float(v), -float(v)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [-float(t[1]), float(t[0])]
 
 
 def bc7_secondary(args, gic, src, size, avail_rows, world, dev, rank, shake_ranks=0, ref_rows=None, bound=0.0):
@@ -222,19 +244,22 @@ def bc7_secondary(args, gic, src, size, avail_rows, world, dev, rank, shake_rank
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    t = _max_over_ranks(torch.tensor([wall, ev0.elapsed_time(ev1)], dtype=torch.float64, device=dev), world)
+    own = ev0.elapsed_time(ev1)
+    t = _max_over_ranks(torch.tensor([wall, own], dtype=torch.float64, device=dev), world)
     wall, kern_ms = float(t[0]), float(t[1])
+    spread = _spread_over_ranks(own, world)
     px = size * rows * 4 * world
     search = "exact (reference search, bit-identical)" if shake_ranks == 0 else \
         f"pruned: {shake_ranks} partitions shaken per mode (per-block MSE tolerance)"
     if bound > 0:
-        search = (f"bounded exit: blocks whose mode-6/3/1 probe decodes within MSE {bound:g} are final "
-                  f"(contract met by construction), the rest " +
-                  ("the exact search" if shake_ranks == 0 else f"the pruned search ({shake_ranks} partitions)"))
+        search = (f"bounded exit: blocks whose mode-6/3/1 probe decodes within MSE {bound:g} are final, the rest " +
+                  ("the exact search (contract met by construction)" if shake_ranks == 0 else
+                   f"the pruned search ({shake_ranks} partitions; contract checked on a sample)"))
     res = {"metric": f"Mpixels/s BC7 quality {args.bc7_quality:g} (all modes, shakers on), {search}",
            "value": round(px / wall / 1e6, 4), "unit": "Mpixels/s",
            "blocks_per_s": round(bx * rows * world / wall, 1), "ms_per_pass": round(wall * 1e3, 2),
-           "kernel_ms": round(kern_ms, 2), "rows_per_gpu": rows * 4, "dtype": "f64+int32",
+           "kernel_ms": round(kern_ms, 2), "kernel_ms_rank_min_max": [round(x, 2) for x in spread],
+           "rows_per_gpu": rows * 4, "dtype": "f64+int32",
            "roofline": {"bound": "valu", "alg_bytes_per_launch": 80 * bx * rows,
                         "hbm_frac": round(80 * bx * rows / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 8)}}
     if rank == 0 and not args.no_cpu and ref_rows is not None:
@@ -290,7 +315,9 @@ def _timed(world, dev, stream, fn, steps):
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    t = _max_over_ranks(torch.tensor([wall, ev0.elapsed_time(ev1) / steps], dtype=torch.float64, device=dev), world)
+    own = ev0.elapsed_time(ev1) / steps
+    t = _max_over_ranks(torch.tensor([wall, own], dtype=torch.float64, device=dev), world)
+    _timed.spread = _spread_over_ranks(own, world)
     return float(t[0]), float(t[1])
 
 
@@ -317,6 +344,7 @@ def bc45_leg(args, gic, fmt, world, dev, rank):
     res = {"metric": f"Mpixels/s {'BC4 R8 height' if fmt == 4 else 'BC5 RG8 normal'} {size}x{size}",
            "value": round(size * size * world * args.steps / wall / 1e6, 3), "unit": "Mpixels/s",
            "ms_per_step": round(wall / args.steps * 1e3, 4), "kernel_ms": round(kern_ms, 4),
+           "kernel_ms_rank_min_max": [round(x, 4) for x in _timed.spread],
            "roofline": {"bound": "hbm", "achieved": round(alg / (kern_ms * 1e-3) / 1e9, 3), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(alg / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
                         "alg_bytes_per_launch": alg}}
@@ -329,10 +357,16 @@ def bc45_leg(args, gic, fmt, world, dev, rank):
         c0 = time.perf_counter()
         ref = oracle_lib.encode_image(fmt, host, bc4_channel=0, first_row=0, num_rows=rows, threads=threads)
         dt = time.perf_counter() - c0
+        budget = args.cpu_seconds / 2   # grow the sample to ~budget s of CPU work, bounded by the image
+        if dt < budget / 4 and rows < by:
+            rows = int(min(by, max(rows, rows * budget / max(dt, 1e-3))))
+            c0 = time.perf_counter()
+            ref = oracle_lib.encode_image(fmt, host, bc4_channel=0, first_row=0, num_rows=rows, threads=threads)
+            dt = time.perf_counter() - c0
         got = dst.cpu().numpy().reshape(-1, gic.block_bytes(fmt))[:rows * bx]
         res["cpu_baseline"] = {"value": round(rows * 4 * size / dt / 1e6, 4), "unit": "Mpixels/s",
                                "cores": threads, "kind": "port", "cpu_model": cpu_model(),
-                               "sample": f"block rows 0-{rows - 1} ({rows * bx} blocks, {dt:.2f} s)"}
+                               "sample": f"block rows 0-{rows - 1} ({rows * bx} blocks, {dt:.2f} s, {threads} threads)"}
         res["gpu_parity"] = "bit-exact" if np.array_equal(got, ref) else \
             f"{int((got != ref).any(axis=1).sum())} blocks differ"
     return res
@@ -361,6 +395,7 @@ def bc7enc16_leg(args, gic, src, size, world, dev, rank, fast):
            "value": round(size * size * world * args.steps / wall / 1e6, 3), "unit": "Mpixels/s",
            "blocks_per_s": round(bx * by * world * args.steps / wall, 1),
            "ms_per_step": round(wall / args.steps * 1e3, 4), "kernel_ms": round(kern_ms, 4), "dtype": "f32+int32",
+           "kernel_ms_rank_min_max": [round(x, 4) for x in _timed.spread],
            "roofline": {"bound": "valu", "achieved": round(alg / (kern_ms * 1e-3) / 1e9, 3), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(alg / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
                         "alg_bytes_per_launch": alg}}
@@ -419,47 +454,43 @@ def _cpu_threads():
 def batch_workload(args, gic, world, rank, dev):
     """configs[4]: BC7 (quality 1) over a fixed stack of S G1 slices (slice s
     seeded 0x9E3779B9+s), every slice's block rows split over the ranks
-    (shard.shard_rows, strong scaling: the batch is fixed, each rank does 1/N);
-    a step = one gic_hip_encode_rows call over the rank's rows of all slices.
-    After the timed steps one RCCL all-gather brings every shard to every rank
-    and rank 0 restores the reference block order, timed separately."""
+    (strong scaling: the batch is fixed, each rank does 1/N) in chunks of
+    --shard-chunk rows dealt round-robin (shard.row_ranges; 0 = contiguous);
+    a step = the rank's gic_hip_encode_rows calls (one per range, every slice
+    at once).  After the timed steps one gather (RCCL on GPUs) brings every
+    shard to rank 0, which restores the reference block order, timed
+    separately."""
     import numpy as np
     import torch
     import torch.distributed as dist
     from gfx_imagecompress_amd import shard, synth
     S, n = args.batch_slices, args.batch_size
     bx = by = (n + 3) // 4
-    first, rows = shard.shard_rows(by, world, rank)
+    chunk = args.shard_chunk
+    ranges = shard.row_ranges(by, world, rank, chunk)
+    nblk = shard.shard_blocks(by, bx, S, world, rank, chunk)
     src = synth.g1_torch(n, n, S, seed=0x9E3779B9, device=dev)
-    dst = torch.empty(max(1, S * rows * bx * 16), dtype=torch.uint8, device=dev)
+    dst = torch.empty(max(1, nblk * 16), dtype=torch.uint8, device=dev)
     opts = gic.Options(bc7_quality=args.bc7_quality, bc7_shake_ranks=args.bc7_shake_ranks,
                        bc7_mse_bound=args.bc7_mse_bound)
     stream = torch.cuda.current_stream(dev)
     # warm-up: the per-device tables and workspaces (one block row of one slice)
-    gic.encode_device(7, src[:1], n, n, 1, 4, dst, opts, first, 1, stream=stream)
-    for _ in range(args.warmup):
-        gic.encode_device(7, src, n, n, S, 4, dst, opts, first, rows, stream=stream)
+    if ranges:
+        gic.encode_device(7, src[:1], n, n, 1, 4, dst, opts, ranges[0][0], 1, stream=stream)
 
     def step():
-        gic.encode_device(7, src, n, n, S, 4, dst, opts, first, rows, stream=stream)
+        shard.encode_shard(7, src, n, n, S, 4, rank, world, opts, stream=stream, chunk=chunk, dst=dst)
+    for _ in range(args.warmup):
+        step()
     wall, kern_ms = _timed(world, dev, stream, step, args.steps)
+    spread = _timed.spread
     gather_ms = None
     full = dst
     if world > 1:
         torch.cuda.synchronize(dev)
         dist.barrier()
         g0 = time.perf_counter()
-        if dist.get_backend() == "gloo":
-            parts = [torch.empty(shard.shard_rows(by, world, r)[1] * bx * S * 16, dtype=torch.uint8)
-                     for r in range(world)]
-            most = max(p.numel() for p in parts)
-            buf = [torch.empty(most, dtype=torch.uint8) for _ in range(world)]
-            loc = torch.zeros(most, dtype=torch.uint8)
-            loc[:dst.numel()] = dst.cpu()[:S * rows * bx * 16]
-            dist.all_gather(buf, loc)
-            full = shard.assemble([b[:p.numel()] for b, p in zip(buf, parts)], 7, n, n, S)
-        else:
-            full = shard.gather_blocks(dst[:S * rows * bx * 16], 7, n, n, S, world)
+        full = shard.gather_to_root(dst[:nblk * 16], 7, n, n, S, world, chunk=chunk)
         torch.cuda.synchronize(dev)
         gather_ms = (time.perf_counter() - g0) * 1e3
         g = _max_over_ranks(torch.tensor([gather_ms], dtype=torch.float64, device=dev), world)
@@ -467,6 +498,13 @@ def batch_workload(args, gic, world, rank, dev):
     total_blocks = S * bx * by
     line = None
     if rank == 0:
+        how = ("one contiguous range per rank" if not chunk else
+               f"chunks of {chunk} block rows dealt round-robin")
+        if world == 1:
+            gather = "one rank: no gather"
+        else:
+            gather = (f"{'RCCL' if dist.get_backend() != 'gloo' else 'gloo (rehearsal)'} gather to rank 0 "
+                      f"timed separately")
         line = {
             "metric": "Mpixels/s (and blocks/s) BC1 & BC7 on 8K RGBA8 at 1/2/4/8 MI355X",
             "value": round(S * n * n * args.steps / wall / 1e6, 4),
@@ -475,28 +513,28 @@ def batch_workload(args, gic, world, rank, dev):
             "vs_baseline": None, "dtype": "f64+int32", "data": "synthetic",
             "config": {"workload": f"configs[4]: BC7 quality {args.bc7_quality:g} on a batch of {S}x{n}x{n} "
                                    f"RGBA8 G1 slices (seed 0x9E3779B9+s), block rows of every slice split over "
-                                   f"{world} rank(s), "
-                                   f"{'RCCL' if world == 1 or dist.get_backend() != 'gloo' else 'gloo (rehearsal)'} "
-                                   f"all-gather to rank 0 timed separately",
+                                   f"{world} rank(s) ({how}), {gather}",
                        "format": "BC7", "slices": S, "width": n, "global_batch_blocks": total_blocks,
                        "bc7_search": ("exact" if args.bc7_shake_ranks == 0 else
                                       f"pruned, {args.bc7_shake_ranks} partitions shaken per mode "
                                       f"(per-block MSE tolerance)") +
                                      (f"; bounded exit: blocks whose mode-6/3/1 probe decodes within MSE "
                                       f"{args.bc7_mse_bound:g} are final" if args.bc7_mse_bound > 0 else ""),
-                       "parallelism": f"block-row shards x{world}",
+                       "parallelism": f"block-row shards x{world}", "shard_chunk_rows": chunk,
                        "world_size_seen": dist.get_world_size() if world > 1 else 1},
             "blocks_per_s": round(total_blocks * args.steps / wall, 1),
             "kernel_ms": round(kern_ms, 3),
+            "kernel_ms_rank_min_max": [round(x, 3) for x in spread],
             "gather_ms": None if gather_ms is None else round(gather_ms, 3),
-            "roofline": {"bound": "hbm", "achieved": round(80 * S * rows * bx / (kern_ms * 1e-3) / 1e9, 4),
+            "roofline": {"bound": "hbm", "achieved": round(80 * nblk / (kern_ms * 1e-3) / 1e9, 4),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(80 * S * rows * bx / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 8),
-                         "traffic": None, "alg_bytes_per_launch": 80 * S * rows * bx,
+                         "frac": round(80 * nblk / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 8),
+                         "traffic": None, "alg_bytes_per_launch": 80 * nblk,
                          "note": "VALU bound; HBM fraction per BASELINE.json"},
             "cpu_baseline": None,
         }
-        host_rows = full.cpu().numpy().reshape(S, by, bx, 16) if full.numel() == total_blocks * 16 else None
+        host_rows = full.cpu().numpy().reshape(S, by, bx, 16) if full is not None and \
+            full.numel() == total_blocks * 16 else None
         if not args.no_cpu and host_rows is not None:
             sys.path.insert(0, os.path.join(ROOT, "tests"))
             import oracle_lib
@@ -581,16 +619,17 @@ def main():
     for _ in range(args.warmup):
         step()
     wall, kern_ms = _timed(world, dev, stream, step, args.steps)
+    spread = _timed.spread
 
     gather_ms = None
     if args.gather and world > 1:
         torch.cuda.synchronize(dev)
         dist.barrier()
         g0 = time.perf_counter()
-        out_all = _gather_all(dst, world)
+        out_all = _gather_root(dst, world)
         torch.cuda.synchronize(dev)
         gather_ms = (time.perf_counter() - g0) * 1e3
-        if out_all.numel() != world * dst.numel():
+        if out_all is not None and out_all.numel() != world * dst.numel():
             raise RuntimeError("gather returned a wrong size")
 
     pixels = size * rows * 4 * world          # pixels encoded per step, all ranks
@@ -666,6 +705,7 @@ def main():
                        "world_size_seen": dist.get_world_size() if world > 1 else 1},
             "blocks_per_s": round(nblocks * world * args.steps / wall, 1),
             "kernel_ms": round(kern_ms, 4),
+            "kernel_ms_rank_min_max": [round(x, 4) for x in spread],
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes,

@@ -268,16 +268,18 @@ extern "C" int gic_hip_encode_blocks_f32(gic_format fmt, const float *d_blocks, 
     if (rc) return rc;
     hipStream_t s = (hipStream_t)stream;
     hipError_t e = hipSuccess;
+    // formats without an encoder error report 0 per block, as the row entries do
+    if (d_block_err && fmt != GIC_FMT_BC7) e = hipMemsetAsync(d_block_err, 0, sizeof(double) * n, s);
+    if (e != hipSuccess) return hip_fail(e);
     if (fmt == GIC_FMT_BC1)
         e = gic::launch_bc1_blocks(d_blocks, n, o.bc1_alpha_threshold, o.refinement_steps, o.b3d_refinement, d_dst, s);
     else if (fmt == GIC_FMT_BC4)
         e = gic::launch_bc4_blocks(d_blocks, n, d_dst, s);
     else if (fmt == GIC_FMT_BC2 || fmt == GIC_FMT_BC3)
         e = gic::launch_bc23_blocks(d_blocks, n, (int)fmt, o.refinement_steps, o.b3d_refinement, d_dst, s);
-    else if (fmt == GIC_FMT_BC7ENC16) {
-        e = d_block_err ? hipMemsetAsync(d_block_err, 0, sizeof(double) * n, s) : hipSuccess;
-        if (e == hipSuccess) e = gic::launch_bc7enc_blocks_f32(d_blocks, n, o, d_dst, s);
-    } else
+    else if (fmt == GIC_FMT_BC7ENC16)
+        e = gic::launch_bc7enc_blocks_f32(d_blocks, n, o, d_dst, s);
+    else
         e = gic::launch_bc7_blocks(d_blocks, n, o, d_dst, d_block_err, s);
     if (e != hipSuccess) return hip_fail(e);
     return GIC_OK;
@@ -788,10 +790,10 @@ extern "C" int gic_save_dds(Image_ImageHeader const *img, const char *path)
     uint32_t h[31];
     memset(h, 0, sizeof(h));
     h[0] = 124;                                   // dwSize
-    h[1] = 0x1 | 0x2 | 0x4 | 0x1000 | 0x80000;    // CAPS | HEIGHT | WIDTH | PIXELFORMAT | LINEARSIZE
+    h[1] = 0x1 | 0x2 | 0x4 | 0x1000 | 0x20000 | 0x80000;   // CAPS | HEIGHT | WIDTH | PIXELFORMAT | MIPMAPCOUNT | LINEARSIZE
     h[2] = img->height;
     h[3] = img->width;
-    h[4] = bx * bb;                               // pitch of a block row
+    h[4] = bx * by * bb;                          // LINEARSIZE: bytes of the top-level image (one slice)
     h[6] = 1;                                     // mip levels
     h[18] = 32;                                   // DDS_PIXELFORMAT.dwSize
     h[19] = 0x4;                                  // DDPF_FOURCC

@@ -46,7 +46,7 @@ typedef struct Image_CompressBC1Options {                                   /* r
 } Image_CompressBC1Options;
 
 typedef struct Image_CompressAMDBackendOptions {                            /* ref :40-45 */
-    bool b3DRefinement;          /* default false (true: unsupported, call fails) */
+    bool b3DRefinement;          /* default false (true: Refine3D, BC1/BC2/BC3) */
     bool AdaptiveColourWeights;  /* default false (true: unsupported, call fails) */
     uint8_t RefinementSteps;     /* default 1 */
     uint8_t ModeMask;            /* default 0xFF (BC7) */

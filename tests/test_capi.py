@@ -112,7 +112,10 @@ def test_dds_writer_headers(tmp_path):
         data = open(path, "rb").read()
         assert data[:4] == b"DDS "
         size, flags, h, w, pitch = struct.unpack_from("<5I", data, 4)
-        assert (size, h, w, pitch) == (124, 12, 20, 5 * bb)
+        # DDSD_LINEARSIZE: total bytes of the top-level image; DDSD_MIPMAPCOUNT with one level
+        assert (size, h, w, pitch) == (124, 12, 20, 5 * 3 * bb)
+        assert flags & 0x80000 and flags & 0x20000
+        assert struct.unpack_from("<I", data, 4 + 24)[0] == 1
         assert data[4 + 80:4 + 84] == want_fourcc
         off = 128
         if dxgi is not None:

@@ -1,8 +1,9 @@
 """Multi-rank block-row sharding on CPU (gloo, world size 2).
 
 Each rank encodes its shard of a 2-slice image whose block-row count does not
-divide evenly, the shards are all-gathered and reassembled, and the result must
-equal the single-process encode byte for byte.  The per-shard encoder here is
+divide evenly (contiguous and interleaved row chunks), the shards are gathered
+to rank 0 and reassembled, and the result must equal the single-process encode
+byte for byte.  The per-shard encoder here is
 the CPU checker (oracle) with the product encoder's signature: this test covers
 the sharding, padding, gather and reassembly logic that bench.py and the
 multi-GPU path use; the HIP encoder itself is covered by the -m gpu tests.
@@ -36,6 +37,25 @@ def test_shard_rows_partition():
         shard.shard_rows(4, 2, 2)
 
 
+def test_row_ranges_partition():
+    """Contiguous and interleaved assignments cover every block row exactly once."""
+    for by in range(0, 70):
+        for world in range(1, 9):
+            for chunk in (0, 1, 3, 16):
+                seen = []
+                for r in range(world):
+                    rr = shard.row_ranges(by, world, r, chunk)
+                    for first, n in rr:
+                        assert n > 0 and (chunk == 0 or world == 1 or n <= chunk)
+                        seen.extend(range(first, first + n))
+                    assert shard.shard_blocks(by, 5, 2, world, r, chunk) == sum(n for _, n in rr) * 10
+                assert sorted(seen) == list(range(by))
+    assert shard.row_ranges(40, 4, 1, 4) == [(4, 4), (20, 4), (36, 4)]
+    assert shard.row_ranges(10, 2, 1, 4) == [(4, 4)]
+    assert shard.row_ranges(10, 2, 0, 4) == [(0, 4), (8, 2)]
+    assert shard.row_ranges(10, 1, 0, 4) == [(0, 10)]   # one rank: one range
+
+
 def _oracle_encoder(fmt, src, width, height, slices, channels, dst, options, first_block_row, num_block_rows,
                     stream=None):
     import oracle_lib
@@ -59,10 +79,11 @@ def _bench_worker(rank, world, port, q):
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
         t = bench._max_over_ranks(torch.tensor([1.0 + rank, 10.0 - rank], dtype=torch.float64), world)
-        g = bench._gather_all(torch.full((5,), rank + 1, dtype=torch.uint8), world)
+        g = bench._gather_root(torch.full((5,), rank + 1, dtype=torch.uint8), world)
+        spread = bench._spread_over_ranks(3.0 + rank, world)
         dist.barrier()
         dist.destroy_process_group()
-        q.put((rank, (t.tolist(), g.tolist())))
+        q.put((rank, (t.tolist(), None if g is None else g.tolist(), spread)))
     except Exception as e:   # pragma: no cover
         q.put((rank, repr(e)))
 
@@ -81,9 +102,11 @@ def test_bench_reductions_two_ranks():
         p.join(timeout=60)
     for r in range(world):
         assert not isinstance(got[r], str), got[r]
-        t, g = got[r]
+        t, g, spread = got[r]
         assert t == [2.0, 10.0]
-        assert g == [1] * 5 + [2] * 5
+        assert spread == [3.0, 4.0]
+        # gather to the root only
+        assert g == ([1] * 5 + [2] * 5 if r == 0 else None)
 
 
 def _worker(rank, world, port, q):
@@ -96,9 +119,10 @@ def _worker(rank, world, port, q):
         for fmt, ch in FMT_CASES:
             img, w, h, s = _image(fmt, ch)
             src = torch.from_numpy(img.reshape(-1))
-            local = shard.encode_shard(fmt, src, w, h, s, ch, rank, world, encoder=_oracle_encoder)
-            full = shard.gather_blocks(local, fmt, w, h, s, world)
-            res.append((fmt, full.numpy().tobytes(), local.numel()))
+            for chunk in (0, 1, 2):
+                local = shard.encode_shard(fmt, src, w, h, s, ch, rank, world, encoder=_oracle_encoder, chunk=chunk)
+                full = shard.gather_to_root(local, fmt, w, h, s, world, chunk=chunk)
+                res.append((fmt, chunk, None if full is None else full.numpy().tobytes(), local.numel()))
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, res))
@@ -129,11 +153,15 @@ def test_two_rank_shards_reassemble_to_single_process_encode():
     for i, (fmt, ch) in enumerate(FMT_CASES):
         img, w, h, s = _image(fmt, ch)
         ref = oracle_lib.encode_image(fmt, img, bc4_channel=0, threads=2).reshape(-1).tobytes()
-        assert got[0][i][1] == ref, fmt
-        assert got[1][i][1] == ref, fmt
-        # uneven split: 3 + 2 block rows of 9 blocks, 2 slices
         bb = 8 if fmt == 1 else 16
-        assert got[0][i][2] == 3 * 9 * 2 * bb and got[1][i][2] == 2 * 9 * 2 * bb
+        # rows per rank: contiguous 3 + 2; chunks of 1 -> {0,2,4} + {1,3}; chunks of 2 -> {0,1,4} + {2,3}
+        for j, chunk in enumerate((0, 1, 2)):
+            fmt0, chunk0, full0, n0 = got[0][3 * i + j]
+            fmt1, chunk1, full1, n1 = got[1][3 * i + j]
+            assert (fmt0, chunk0) == (fmt, chunk) == (fmt1, chunk1)
+            assert full0 == ref, (fmt, chunk)      # reassembled on the root
+            assert full1 is None                   # gather to the root only
+            assert n0 == 3 * 9 * 2 * bb and n1 == 2 * 9 * 2 * bb
 
 
 def test_bench_gpus_flag_launches_ranks(monkeypatch):
