@@ -20,7 +20,8 @@ import os
 from dataclasses import dataclass, replace
 
 __all__ = [
-    "GicError", "Options", "FMT_BC1", "FMT_BC2", "FMT_BC3", "FMT_BC4", "FMT_BC5", "FMT_BC7", "FMT_BC7ENC16",
+    "GicError", "Options", "FMT_BC1", "FMT_BC2", "FMT_BC3", "FMT_BC4", "FMT_BC5", "FMT_BC6H", "FMT_BC6H_SF",
+    "FMT_BC7", "FMT_BC7ENC16", "compress_bc6h",
     "library", "encode_blocks_u8", "compress_bc7_fast",
     "block_bytes", "blocks_shape", "encode_device", "encode_device_src", "encode_blocks_f32", "decode_device", "compress_bc1", "compress_bc2",
     "compress_bc3", "compress_bc4", "compress_bc5", "compress_bc7", "LIB_PATH",
@@ -28,6 +29,7 @@ __all__ = [
 
 FMT_BC1, FMT_BC2, FMT_BC3, FMT_BC4, FMT_BC5, FMT_BC7 = 1, 2, 3, 4, 5, 7
 FMT_BC7ENC16 = 8   # BC7 by bc7enc16, the reference's fast encoder (richgel999_bc7enc16.cpp)
+FMT_BC6H, FMT_BC6H_SF = 6, 9   # BC6H unsigned / signed half floats (amd_bc6h_body.cpp, BC6HBlockEncoder)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GIC_LIBRARY") or os.path.join(_HERE, "lib", "libgfx_imagecompress_amd.so")
 
@@ -261,8 +263,9 @@ def encode_blocks_f32(fmt: int, blocks, dst, options: Options | None = None, blo
     ``Image_CompressAMDMultiModeLDRBlock`` (reference imagecompress.h:117-136).
     """
     import torch
-    if fmt not in (FMT_BC1, FMT_BC2, FMT_BC3, FMT_BC4, FMT_BC7, FMT_BC7ENC16):
-        raise GicError(f"encode_blocks_f32: format {fmt} has no block-level entry (BC1, BC2, BC3, BC4, BC7, BC7ENC16)")
+    if fmt not in (FMT_BC1, FMT_BC2, FMT_BC3, FMT_BC4, FMT_BC6H, FMT_BC6H_SF, FMT_BC7, FMT_BC7ENC16):
+        raise GicError(f"encode_blocks_f32: format {fmt} has no block-level entry "
+                       f"(BC1, BC2, BC3, BC4, BC6H, BC6H_SF, BC7, BC7ENC16)")
     if not (blocks.is_cuda and dst.is_cuda):
         raise GicError("encode_blocks_f32 needs device (HBM) tensors; there is no CPU path")
     if blocks.dtype != torch.float32 or not blocks.is_contiguous():
@@ -382,6 +385,29 @@ def compress_bc7(image, options: Options | None = None):
     if image.ndim >= 3 and image.shape[-1] < 4:
         o = replace(o, force_alpha_one=True)
     return _host_compress(FMT_BC7, image, o)
+
+
+def compress_bc6h(image, signed: bool = False):
+    """Image_CompressAMDBC6H (amd_bc6h_compressor.cpp:11-56) on a host float32
+    array (H,W,C) or (S,H,W,C): BC6H unsigned (signed=False, DXBC6H_UFLOAT) or
+    signed (the encoder's path for signed sources, DXBC6H_SFLOAT).  Returns
+    (S,by,bx,16) uint8 blocks."""
+    import numpy as np
+    import torch
+    a = np.ascontiguousarray(image, dtype=np.float32)
+    if a.ndim == 2:
+        a = a[:, :, None]
+    if a.ndim == 3:
+        a = a[None]
+    s, h, w, c = a.shape
+    bx, by = blocks_shape(w, h)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    src = torch.from_numpy(a).to(dev)
+    dst = torch.empty(bx * by * s * 16, dtype=torch.uint8, device=dev)
+    encode_device_src(FMT_BC6H_SF if signed else FMT_BC6H, SRC_FLOAT32, src.reshape(-1), w, h, s, c, dst,
+                      Options(force_alpha_one=c < 4))
+    torch.cuda.synchronize()
+    return dst.cpu().numpy().reshape(s, by, bx, 16)
 
 
 def compress_bc7_fast(image, options: Options | None = None):

@@ -45,7 +45,14 @@ hipError_t launch_bc7_blocks(const float *blocks, uint32_t n, const gic_options 
 hipError_t launch_bc7enc_image(const Geometry &g, const gic_options &o, void *dst, hipStream_t s);
 hipError_t launch_bc7enc_blocks_u8(const uint32_t *blocks, uint32_t n, const gic_options &o, void *dst, hipStream_t s);
 hipError_t launch_bc7enc_blocks_f32(const float *blocks, uint32_t n, const gic_options &o, void *dst, hipStream_t s);
+hipError_t launch_bc6h_blocks(const float *blocks, uint32_t n, int is_signed, void *dst, double *err, hipStream_t s);
+hipError_t launch_bc6h_image(const Geometry &g, int is_signed, int force_alpha_one, void *dst, double *err,
+                             hipStream_t s);
 }  // namespace gic
+
+static bool is_bc6h(gic_format f) { return f == GIC_FMT_BC6H || f == GIC_FMT_BC6H_SF; }
+// formats whose encoders report a per-block error (others write 0)
+static bool has_error(gic_format f) { return f == GIC_FMT_BC7 || is_bc6h(f); }
 
 static thread_local int t_last_hip_error = 0;
 
@@ -101,7 +108,7 @@ static int check_options(gic_format fmt, const gic_options &o)
 static bool valid_fmt(gic_format f)
 {
     return f == GIC_FMT_BC1 || f == GIC_FMT_BC2 || f == GIC_FMT_BC3 || f == GIC_FMT_BC4 || f == GIC_FMT_BC5 ||
-           f == GIC_FMT_BC7 || f == GIC_FMT_BC7ENC16;
+           f == GIC_FMT_BC7 || f == GIC_FMT_BC7ENC16 || is_bc6h(f);
 }
 
 extern "C" int gic_hip_encode_rows(gic_format fmt, const uint8_t *d_src, uint32_t width, uint32_t height,
@@ -138,7 +145,7 @@ extern "C" int gic_hip_encode_rows(gic_format fmt, const uint8_t *d_src, uint32_
     g.total = (uint32_t)total;
     hipStream_t s = (hipStream_t)stream;
     hipError_t e = hipSuccess;
-    if (d_block_err && fmt != GIC_FMT_BC7) {   // no encoder error but the AMD BC7 one
+    if (d_block_err && !has_error(fmt)) {   // no encoder error but the AMD BC7 / BC6H ones
         e = hipMemsetAsync(d_block_err, 0, sizeof(double) * total, s);
         if (e != hipSuccess) return hip_fail(e);
     }
@@ -160,6 +167,12 @@ extern "C" int gic_hip_encode_rows(gic_format fmt, const uint8_t *d_src, uint32_
         break;
     case GIC_FMT_BC7ENC16:
         e = gic::launch_bc7enc_image(g, o, d_dst, s);
+        break;
+    case GIC_FMT_BC6H:
+    case GIC_FMT_BC6H_SF:
+        e = gic::launch_bc6h_image(g, fmt == GIC_FMT_BC6H_SF, o.force_alpha_one, d_dst, d_block_err, s);
+        break;
+    default:
         break;
     }
     if (e != hipSuccess) return hip_fail(e);
@@ -208,7 +221,7 @@ extern "C" int gic_hip_encode_rows_src(gic_format fmt, gic_source src_type, cons
     float *tmp = nullptr;
     hipError_t e = hipMallocAsync((void **)&tmp, (size_t)chunk * 64 * sizeof(float), s);
     if (e != hipSuccess) return hip_fail(e);
-    if (d_block_err && fmt != GIC_FMT_BC7) e = hipMemsetAsync(d_block_err, 0, sizeof(double) * total, s);
+    if (d_block_err && !has_error(fmt)) e = hipMemsetAsync(d_block_err, 0, sizeof(double) * total, s);
     const uint32_t bb = gic_block_bytes(fmt);
     const int force_alpha = o.force_alpha_one || channels < 4;
     for (uint32_t first = 0; e == hipSuccess && first < (uint32_t)total; first += chunk) {
@@ -234,6 +247,13 @@ extern "C" int gic_hip_encode_rows_src(gic_format fmt, gic_source src_type, cons
         case GIC_FMT_BC7ENC16:
             e = gic::launch_bc7enc_blocks_f32(tmp, n, o, out, s);
             break;
+        case GIC_FMT_BC6H:
+        case GIC_FMT_BC6H_SF:
+            e = gic::launch_bc6h_blocks(tmp, n, fmt == GIC_FMT_BC6H_SF, out, d_block_err ? d_block_err + first : nullptr,
+                                        s);
+            break;
+        default:
+            break;
         }
     }
     const hipError_t ef = hipFreeAsync(tmp, s);
@@ -256,7 +276,7 @@ extern "C" int gic_hip_encode_blocks_f32(gic_format fmt, const float *d_blocks, 
 {
     if (!d_blocks || !d_dst || !n) return GIC_EINVAL;
     if (fmt != GIC_FMT_BC1 && fmt != GIC_FMT_BC2 && fmt != GIC_FMT_BC3 && fmt != GIC_FMT_BC4 && fmt != GIC_FMT_BC7 &&
-        fmt != GIC_FMT_BC7ENC16)
+        fmt != GIC_FMT_BC7ENC16 && !is_bc6h(fmt))
         return GIC_EINVAL;
     gic_options o;
     gic_default_options(&o);
@@ -269,9 +289,11 @@ extern "C" int gic_hip_encode_blocks_f32(gic_format fmt, const float *d_blocks, 
     hipStream_t s = (hipStream_t)stream;
     hipError_t e = hipSuccess;
     // formats without an encoder error report 0 per block, as the row entries do
-    if (d_block_err && fmt != GIC_FMT_BC7) e = hipMemsetAsync(d_block_err, 0, sizeof(double) * n, s);
+    if (d_block_err && !has_error(fmt)) e = hipMemsetAsync(d_block_err, 0, sizeof(double) * n, s);
     if (e != hipSuccess) return hip_fail(e);
-    if (fmt == GIC_FMT_BC1)
+    if (is_bc6h(fmt))
+        e = gic::launch_bc6h_blocks(d_blocks, n, fmt == GIC_FMT_BC6H_SF, d_dst, d_block_err, s);
+    else if (fmt == GIC_FMT_BC1)
         e = gic::launch_bc1_blocks(d_blocks, n, o.bc1_alpha_threshold, o.refinement_steps, o.b3d_refinement, d_dst, s);
     else if (fmt == GIC_FMT_BC4)
         e = gic::launch_bc4_blocks(d_blocks, n, d_dst, s);
@@ -305,7 +327,7 @@ extern "C" int gic_hip_encode_blocks_u8(gic_format fmt, const uint32_t *d_blocks
 extern "C" int gic_hip_decode(gic_format fmt, const uint8_t *d_blocks, uint32_t width, uint32_t height,
                               uint32_t slices, uint8_t *d_rgba, size_t row_pitch, void *stream)
 {
-    if (!valid_fmt(fmt) || !d_blocks || !d_rgba || !width || !height || !slices) return GIC_EINVAL;
+    if (!valid_fmt(fmt) || is_bc6h(fmt) || !d_blocks || !d_rgba || !width || !height || !slices) return GIC_EINVAL;
     if (row_pitch < (size_t)width * 4) return GIC_EINVAL;
     const hipError_t e = (fmt == GIC_FMT_BC7 || fmt == GIC_FMT_BC7ENC16)
                              ? gic::launch_bc7_decode(d_blocks, width, height, slices, d_rgba, row_pitch, (hipStream_t)stream)
@@ -345,6 +367,8 @@ extern "C" uint32_t TinyImageFormat_ChannelCount(TinyImageFormat f)
     case TinyImageFormat_DXBC3_SRGB:
     case TinyImageFormat_DXBC7_UNORM:
     case TinyImageFormat_DXBC7_SRGB: return 4;
+    case TinyImageFormat_DXBC6H_UFLOAT:
+    case TinyImageFormat_DXBC6H_SFLOAT: return 3;
     default: return 0;
     }
 }
@@ -359,10 +383,15 @@ extern "C" bool TinyImageFormat_IsSRGB(TinyImageFormat f)
 extern "C" bool TinyImageFormat_IsSigned(TinyImageFormat f)
 {
     return f == TinyImageFormat_R8_SNORM || f == TinyImageFormat_R8G8_SNORM || f == TinyImageFormat_DXBC4_SNORM ||
-           f == TinyImageFormat_DXBC5_SNORM || f == TinyImageFormat_R32G32B32A32_SFLOAT;
+           f == TinyImageFormat_DXBC5_SNORM || f == TinyImageFormat_R32G32B32A32_SFLOAT ||
+           f == TinyImageFormat_DXBC6H_SFLOAT;
 }
 
-extern "C" bool TinyImageFormat_IsFloat(TinyImageFormat f) { return f == TinyImageFormat_R32G32B32A32_SFLOAT; }
+extern "C" bool TinyImageFormat_IsFloat(TinyImageFormat f)
+{
+    return f == TinyImageFormat_R32G32B32A32_SFLOAT || f == TinyImageFormat_DXBC6H_UFLOAT ||
+           f == TinyImageFormat_DXBC6H_SFLOAT;
+}
 
 extern "C" bool TinyImageFormat_IsCompressed(TinyImageFormat f) { return f >= TinyImageFormat_DXBC1_RGB_UNORM; }
 
@@ -627,12 +656,21 @@ extern "C" Image_ImageHeader const *Image_CompressAMDBC3(Image_ImageHeader const
     return compress_bc23(src, GIC_FMT_BC3, amd, cb, user);
 }
 
-// Outside this release: BC6H is exported for link
-// compatibility and fails the way the reference reports any failure (NULL).
-extern "C" Image_ImageHeader const *Image_CompressAMDBC6H(Image_ImageHeader const *, Image_CompressAMDBackendOptions const *,
-                                                          Image_CompressProgressFunc, void *)
+// amd_bc6h_compressor.cpp:11-56: signed sources give DXBC6H_SFLOAT and the
+// encoder's signed path, others DXBC6H_UFLOAT; quality 1.0; the ModeMask is
+// passed to a constructor parameter that nothing reads, so it changes nothing.
+extern "C" Image_ImageHeader const *Image_CompressAMDBC6H(Image_ImageHeader const *src,
+                                                          Image_CompressAMDBackendOptions const *amd,
+                                                          Image_CompressProgressFunc cb, void *user)
 {
-    return nullptr;
+    if (!src) return nullptr;
+    (void)amd;
+    const bool sgn = TinyImageFormat_IsSigned(src->format);
+    gic_options o;
+    gic_default_options(&o);
+    o.force_alpha_one = TinyImageFormat_ChannelCount(src->format) > 3 ? 0 : 1;
+    return encode_host_image(src, sgn ? GIC_FMT_BC6H_SF : GIC_FMT_BC6H,
+                             sgn ? TinyImageFormat_DXBC6H_SFLOAT : TinyImageFormat_DXBC6H_UFLOAT, o, cb, user);
 }
 
 // The bc7enc16 options of Image_CompressRichGel999BC7enc16 (richgel999_bc7enc16.cpp:73-89):
@@ -735,6 +773,8 @@ static gic_format block_format_of(TinyImageFormat f)
     case TinyImageFormat_DXBC5_SNORM: return GIC_FMT_BC5;
     case TinyImageFormat_DXBC7_UNORM:
     case TinyImageFormat_DXBC7_SRGB: return GIC_FMT_BC7;
+    case TinyImageFormat_DXBC6H_UFLOAT: return GIC_FMT_BC6H;
+    case TinyImageFormat_DXBC6H_SFLOAT: return GIC_FMT_BC6H_SF;
     default: return (gic_format)0;
     }
 }
@@ -773,7 +813,7 @@ extern "C" int gic_save_dds(Image_ImageHeader const *img, const char *path)
     if (!fmt) return GIC_EINVAL;
     const bool srgb = TinyImageFormat_IsSRGB(img->format);
     const bool snorm = img->format == TinyImageFormat_DXBC4_SNORM || img->format == TinyImageFormat_DXBC5_SNORM;
-    const bool dx10 = fmt == GIC_FMT_BC7 || srgb || snorm || img->slices > 1;
+    const bool dx10 = fmt == GIC_FMT_BC7 || is_bc6h(fmt) || srgb || snorm || img->slices > 1;
     // DXGI_FORMAT values of the DX10 header
     uint32_t dxgi = 0;
     switch (fmt) {
@@ -784,6 +824,8 @@ extern "C" int gic_save_dds(Image_ImageHeader const *img, const char *path)
     case GIC_FMT_BC5: dxgi = snorm ? 84 : 83; break;
     case GIC_FMT_BC7:
     case GIC_FMT_BC7ENC16: dxgi = srgb ? 99 : 98; break;
+    case GIC_FMT_BC6H: dxgi = 95; break;      // DXGI_FORMAT_BC6H_UF16
+    case GIC_FMT_BC6H_SF: dxgi = 96; break;   // DXGI_FORMAT_BC6H_SF16
     }
     const uint32_t bb = gic_block_bytes(fmt);
     const uint32_t bx = (img->width + 3) / 4, by = (img->height + 3) / 4;

@@ -1,0 +1,1276 @@
+// gic_bc6h.hip -- BC6H (HDR) block encoder for gfx950 (MI355X).
+//
+// Algorithm: the reference's BC6HBlockEncoder::CompressBlock at the quality
+// Image_CompressAMDBC6H constructs it with (1.0; src/amd_bc6h_body.cpp:1521-1652,
+// src/amd_bc6h_compressor.cpp:28) and the HDR_Encode helpers it calls
+// (src/amd_hdr_encode.cpp).  Single-precision arithmetic in the reference's
+// operation order (-ffp-contract=off, correctly rounded divide / sqrt), so the
+// output is bit-identical to the CPU restatement oracle/orc_bc6h.c, which
+// states every quirk this file reproduces (the one-region pattern never being
+// encoded, the always-unsigned end point decode, QuantizeToInt on the
+// unclamped value, ep_shaker_HD's single round on 8-bit codes, ...).
+//
+// Mapping (a chunk of blocks per pass):
+//   K1 k_bc6h_pattern   1 lane / (block, pattern): FindBestPattern (:904-1037)
+//                       for the one-region pattern or one of the 32 two-region
+//                       shapes -- optQuantAnD_f per subset (4000 rounds with the
+//                       stale snapshot; cycles are fast-forwarded exactly),
+//                       ep_shaker_HD's 64-corner walk per subset, the clamped
+//                       end points and the pattern's CalcShapeError;
+//   K2 k_bc6h_encode    1 lane / block: the first strictly smaller pattern
+//                       error (shape 31's state when the one-region pattern
+//                       wins, :1621-1631), EncodePattern over modes 1..10
+//                       (:1351-1488) and SaveDataBlock (:125-454).
+// Every per-texel array is held in registers and visited with compile-time
+// indices over a 16-bit subset mask (members in texel order = the
+// reference's compacted subset order); nothing goes through scratch.
+
+#include <mutex>
+
+#include "gic_common.h"
+#include "bc7_tables.h"
+
+namespace gic {
+namespace bc6h {
+
+constexpr int kPatterns = 33;     // 0 = one region, 1 + s = two-region shape s
+constexpr int kF16Max = 0x7bff;   // F16MAX, amd_bc6h_body.hpp:49
+
+__constant__ uint32_t dShape[32];    // BPTC two-subset shapes 0..31, 2 bits per texel
+__constant__ uint8_t dAnchor[32];    // anchor texel of subset 1 (g_indexfixups)
+
+struct PatternState {   // FindBestPattern's result for one (block, pattern)
+    float err;
+    float pad;
+    float fep[12];      // fEndPoints[subset][end][channel] after clampF16Max
+    uint64_t idx;       // shape_indices per texel, 4 bits each
+};
+
+// (int)f with x86 cvttss2si semantics: INT_MIN for NaN and out-of-range
+__device__ __forceinline__ int cvt_i32(float f)
+{
+    return (f >= -2147483648.0f && f < 2147483648.0f) ? (int)f : (int)0x80000000;
+}
+
+// IEEE binary16 round to nearest even (the assumed Math_Float2Half; see orc_bc6h.c)
+__device__ __forceinline__ uint32_t f2h(float f)
+{
+    const uint32_t u = __float_as_uint(f);
+    const uint32_t sign = (u >> 16) & 0x8000u, ex = (u >> 23) & 0xffu;
+    uint32_t man = u & 0x7fffffu;
+    if (ex == 0xffu) return sign | 0x7c00u | (man ? 0x200u : 0u);
+    const int e = (int)ex - 127 + 15;
+    if (e >= 31) return sign | 0x7c00u;
+    if (e <= 0) {
+        if (e < -10) return sign;
+        man |= 0x800000u;
+        const int shift = 14 - e;
+        uint32_t h = man >> shift;
+        const uint32_t rem = man & ((1u << shift) - 1u), half = 1u << (shift - 1);
+        if (rem > half || (rem == half && (h & 1u))) h++;
+        return sign | h;
+    }
+    uint32_t h = ((uint32_t)e << 10) | (man >> 13);
+    const uint32_t rem = man & 0x1fffu;
+    if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) h++;
+    return sign | h;
+}
+
+__device__ __forceinline__ int nib(uint64_t v, int t) { return (int)((v >> (4 * t)) & 15u); }
+__device__ __forceinline__ uint64_t set_nib(uint64_t v, int t, int x)
+{
+    return (v & ~(15ull << (4 * t))) | ((uint64_t)(x & 15) << (4 * t));
+}
+
+// ---------------------------------------------------------- optQuantAnD_f ---
+
+// quant_AnD_Shell (float), amd_hdr_encode.cpp:1349-1425, over the members of
+// `mask`; the fix-up branch keeps the reference's stable qsort via an
+// insertion network on (value, member) keys
+__device__ __forceinline__ void shell_f(const float prj[16], uint32_t mask, int n, int k, int idx[16])
+{
+    float m = 0.f, M = 0.f;
+    bool first = true;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if ((mask >> i) & 1u) {
+            if (first) {
+                m = M = prj[i];
+                first = false;
+            } else {
+                m = m < prj[i] ? m : prj[i];
+                M = M > prj[i] ? M : prj[i];
+            }
+        }
+    if (M == m) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) idx[i] = 0;
+        return;
+    }
+    const float s = (float)(k - 1) / (M - m);
+    float d[16], dm = 0.f, r = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        d[i] = 0.f;
+        if ((mask >> i) & 1u) {
+            const float v = prj[i] * s;
+            const float z = v + 0.5f - m * s;   // not floored (the floor is commented out, :1381)
+            idx[i] = cvt_i32(z);
+            d[i] = v - z - m * s;
+            dm += d[i];
+            r += d[i] * d[i];
+        }
+    }
+    if ((float)n * r - dm * dm >= (float)(n - 1) / 4 / 2) {
+        dm /= (float)n;
+        // members in texel order, then the reference's stable qsort (a_compare:
+        // difference sign) as an insertion sort over the first n entries
+        float key[16];
+        int who[16];
+        int q = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            key[i] = 0.f;
+            who[i] = 0;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if ((mask >> i) & 1u) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    if (j == q) {
+                        key[j] = d[i] - dm;
+                        who[j] = i;
+                    }
+                ++q;
+            }
+#pragma unroll
+        for (int a = 1; a < 16; ++a)
+#pragma unroll
+            for (int b = a; b > 0; --b)
+                if (a < n && key[b - 1] - key[b] > 0) {
+                    const float tk = key[b];
+                    key[b] = key[b - 1];
+                    key[b - 1] = tk;
+                    const int tw = who[b];
+                    who[b] = who[b - 1];
+                    who[b - 1] = tw;
+                }
+        float mm = 0.f, l = 0.f;
+        int j = -1;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (i < n) {
+                key[i] -= (2.0f * (float)i + 1.0f - (float)n) / 2.0f / (float)n;
+                l += key[i];
+                if (l < mm) {
+                    mm = l;
+                    j = i;
+                }
+            }
+        j = (j + 1) % n;
+        uint32_t inc = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (i < n && i >= j) inc |= 1u << who[i];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) idx[i] += (int)((inc >> i) & 1u);
+    }
+    int mi = 0;
+    first = true;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if ((mask >> i) & 1u) {
+            mi = first ? idx[i] : (mi < idx[i] ? mi : idx[i]);
+            first = false;
+        }
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if ((mask >> i) & 1u) idx[i] -= mi;
+}
+
+// eigenVector_d (float), amd_hdr_encode.cpp:1200-1286: p = 5 squarings per
+// round, q = 4 rounds (dimension 3); vec untouched when the matrix is zero
+__device__ __forceinline__ void eigen_f(const float cov[3][3], float vec[3])
+{
+    float a[3][3], b[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) a[i][j] = cov[i][j];
+    for (int n = 0; n < 4; ++n) {
+        float md = 0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) md = a[i][i] > md ? a[i][i] : md;
+        if (md <= 0) return;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) a[i][j] /= md;
+        for (int m = 0; m < 5; ++m) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    float t = 0;
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) t += a[i][k] * a[k][j];
+                    b[i][j] = t;
+                }
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) a[i][j] = b[i][j];
+        }
+    }
+    float md = 0;
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        k = a[i][i] > md ? i : k;
+        md = a[i][i] > md ? a[i][i] : md;
+    }
+    float row[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) row[i] = k == 0 ? a[0][i] : (k == 1 ? a[1][i] : a[2][i]);
+    float t = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        t += row[i] * row[i];
+        vec[i] = row[i];
+    }
+    t = sqrtf(t);
+    if (t <= 0) return;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) vec[i] /= t;
+}
+
+// per-round state hash for the fast-forward (indices of the members, 4 bits each)
+__device__ __forceinline__ uint64_t pack_idx(const int idx[16], uint32_t mask)
+{
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if ((mask >> k) & 1u) v |= (uint64_t)(idx[k] & 15) << (4 * k);
+    return v;
+}
+
+// optQuantAnD_f (amd_hdr_encode.cpp:1427-1601), dimension 3, quality 1.0, over
+// the members of `mask` (data = din, texel-indexed).  Returns the error; idx
+// (texel-indexed) and the GetEndPoints (:1116-1159) end points ep[2][3].
+//
+// The 4000-round loop compares against the it == 1 snapshot only, so a run
+// caught in a cycle that avoids it spins to the end.  The round's state is
+// idx after the shell (plus try_two while it is >= 0; once negative its value
+// no longer matters); a state recurring after P <= 4 rounds repeats with
+// period P and never breaks, so whole periods are skipped -- the final idx is
+// the reference's.  The requantisation sweep over the sorted projections is
+// the count of thresholds (k + 0.5 - s) t (double, :1532) below each
+// projection: the thresholds are non-decreasing in k since t >= 0.
+__device__ __forceinline__ float opt_quant_f(const float din[16][3], uint32_t mask, int ncl, int idx[16], float dir[3],
+                             float ep[2][3])
+{
+    const int n = __popc(mask);
+    float mean[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        float acc = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if ((mask >> k) & 1u) acc += din[k][i];
+        mean[i] = acc / (float)n;
+    }
+    float cov[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) {
+            float acc = 0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if ((mask >> k) & 1u) acc += (din[k][i] - mean[i]) * (din[k][j] - mean[j]);
+            cov[i][j] = acc;
+        }
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = i + 1; j < 3; ++j) cov[i][j] = cov[j][i];
+    eigen_f(cov, dir);
+    float prj[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        prj[k] = 0.f;
+        idx[k] = 0;
+        if ((mask >> k) & 1u) {
+            float acc = 0;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) acc += (din[k][i] - mean[i]) * dir[i];
+            prj[k] = acc;
+        }
+    }
+    uint64_t snap = 0;
+    int try_two = 50;
+    uint64_t seen[4] = {0, 0, 0, 0};
+    int seen_tt[4] = {0, 0, 0, 0};
+    bool ff = true;
+    for (int it = 0; it < 4000; ++it) {
+        if (it >= 2 && ff) {
+            const uint64_t cur = pack_idx(idx, mask);
+            const int tcls = try_two < 0 ? -1 : try_two;
+#pragma unroll
+            for (int P = 1; P <= 4; ++P) {
+                const int h = (it - P) & 3;
+                if (ff && it - P >= 2 && seen[h] == cur && seen_tt[h] == tcls) {
+                    it += ((4000 - it) / P) * P;
+                    ff = false;
+                }
+            }
+            seen[it & 3] = cur;
+            seen_tt[it & 3] = tcls;
+            if (it >= 4000) break;
+        }
+        if (it) {
+            bool done;
+            int inner = 0;
+            do {
+                float q = 0, s = 0, t = 0;
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    if ((mask >> k) & 1u) {
+                        s += (float)idx[k];
+                        t += (float)(idx[k] * idx[k]);
+                    }
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    float acc = 0;
+#pragma unroll
+                    for (int k = 0; k < 16; ++k)
+                        if ((mask >> k) & 1u) acc += (din[k][j] - mean[j]) * (float)idx[k];
+                    dir[j] = acc;
+                    q += dir[j] * dir[j];
+                }
+                s /= (float)n;
+                t = t - s * s * (float)n;
+                t = (t == 0.0f ? 0.0f : 1.0f / t);
+                q = sqrtf(q);
+                t *= q;
+                if (q != 0)
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) dir[j] /= q;
+                done = true;
+                const double ds = (double)s, dt = (double)t;
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    if ((mask >> k) & 1u) {
+                        float acc = 0;
+#pragma unroll
+                        for (int i = 0; i < 3; ++i) acc += (din[k][i] - mean[i]) * dir[i];
+                        prj[k] = acc;
+                        int cnt = 0;
+                        for (int c = 0; c < ncl - 1; ++c) cnt += ((double)acc > ((double)c + 0.5 - ds) * dt) ? 1 : 0;
+                        done = done && cnt == idx[k];
+                        idx[k] = cnt;
+                    }
+                if (++inner > 4096) break;   // the reference loops until done once try_two < 0 (orc_bc6h.c)
+            } while (!done && try_two--);
+            if (it == 1) {
+                snap = pack_idx(idx, mask);
+            } else if (pack_idx(idx, mask) == snap) {
+                break;
+            }
+        }
+        shell_f(prj, mask, n, ncl, idx);
+    }
+    float q = 0, s = 0, t = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if ((mask >> k) & 1u) {
+            s += (float)idx[k];
+            t += (float)(idx[k] * idx[k]);
+        }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        float acc = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if ((mask >> k) & 1u) acc += (din[k][j] - mean[j]) * (float)idx[k];
+        dir[j] = acc;
+        q += dir[j] * dir[j];
+    }
+    s /= (float)n;
+    t = t - s * s * (float)n;
+    t = (t == 0.0f ? 0.0f : 1.0f / t);
+    float err = 0, mn = 65504.0f, mx = 0;
+    int mini = -1, maxi = -1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if ((mask >> i) & 1u) {
+            float o[3];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                o[j] = mean[j] + dir[j] * t * ((float)idx[i] - s);
+                err += (din[i][j] - o[j]) * (din[i][j] - o[j]);
+            }
+            const float val = o[0] + o[1] + o[2];
+            if (mini < 0) mini = maxi = i;   // GetEndPoints' defaults: the first member
+            if (val < mn) {
+                mn = val;
+                mini = i;
+            }
+            if (val > mx) {
+                mx = val;
+                maxi = i;
+            }
+        }
+    // end points = the quantised points of the chosen members (recomputed:
+    // the same expression gives the same floats)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (i == mini)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) ep[0][j] = mean[j] + dir[j] * t * ((float)idx[i] - s);
+        if (i == maxi)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) ep[1][j] = mean[j] + dir[j] * t * ((float)idx[i] - s);
+    }
+    q = sqrtf(q);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) dir[j] /= q;
+    return err;
+}
+
+// ----------------------------------------------------------- ep_shaker_HD ---
+
+__constant__ float kLerpW[5][16] = {
+    {0.0f},
+    {0.0f, 1.0f},
+    {0.0f, 21.0f / 64.0f, 43.0f / 64.0f, 1.0f},
+    {0.0f, 9.0f / 64.0f, 18.0f / 64.0f, 27.0f / 64.0f, 37.0f / 64.0f, 46.0f / 64.0f, 55.0f / 64.0f, 1.0f},
+    {0.0f, 4.0f / 64.0f, 9.0f / 64.0f, 13.0f / 64.0f, 17.0f / 64.0f, 21.0f / 64.0f, 26.0f / 64.0f, 30.0f / 64.0f,
+     34.0f / 64.0f, 38.0f / 64.0f, 43.0f / 64.0f, 47.0f / 64.0f, 51.0f / 64.0f, 55.0f / 64.0f, 60.0f / 64.0f, 1.0f}};
+
+template <int CLOG> struct Lerp;
+template <> struct Lerp<0> { __device__ static float w(int) { return 0.0f; } };
+template <> struct Lerp<1> { __device__ static float w(int i) { return i ? 1.0f : 0.0f; } };
+template <> struct Lerp<2> {
+    __device__ static float w(int i)
+    {
+        return i == 0 ? 0.0f : i == 1 ? 21.0f / 64.0f : i == 2 ? 43.0f / 64.0f : 1.0f;
+    }
+};
+template <> struct Lerp<3> {
+    __device__ static float w(int i)
+    {
+        constexpr float t[8] = {0.0f, 9.0f / 64.0f, 18.0f / 64.0f, 27.0f / 64.0f,
+                                37.0f / 64.0f, 46.0f / 64.0f, 55.0f / 64.0f, 1.0f};
+        return t[i];
+    }
+};
+
+// ep_df / expandbits_ with 8-bit codes (amd_hdr_encode.cpp:2098-2111)
+__device__ __forceinline__ float ep8(int v) { return (float)(v | (v >> 8)); }
+
+// rampf (USE_NEWRAMP, :2113-2120)
+template <int CLOG>
+__device__ __forceinline__ float ramp8(float a, float b, int i)
+{
+    const float ret = floorf(a + Lerp<CLOG>::w(i) * (float)(b - a) + 0.5f);
+    return ret > 256.0f ? 255.0f : ret;
+}
+
+// ep_shaker_HD (amd_hdr_encode.cpp:2280-2614) for one subset, dimension 3,
+// bits {8, 8, 8}, Mi_ = n - 1, CLOG = floor(log2(n)); exactly one round.
+// idx (texel-indexed) is updated in place like the reference's index_.
+template <int CLOG>
+__device__ __forceinline__ float shaker_hd(const float din[16][3], uint32_t mask, int n, int idx[16], int epo[2][3])
+{
+    constexpr int NCL = 1 << CLOG;
+    const int Mi_ = n - 1;
+    bool alls = true;
+    int f0 = -1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if ((mask >> i) & 1u) {
+            if (f0 < 0) f0 = i;
+        }
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if ((mask >> i) & 1u)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                float d0 = din[0][j];
+#pragma unroll
+                for (int u = 1; u < 16; ++u) d0 = u == f0 ? din[u][j] : d0;
+                alls = alls && d0 == din[i][j];
+            }
+    // index_collapse_kernel (:1688-1713)
+    int cidx0[16];
+    int mi = 0x7fffffff, Mx = -0x7fffffff;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if ((mask >> k) & 1u) {
+            mi = mi < idx[k] ? mi : idx[k];
+            Mx = Mx > idx[k] ? Mx : idx[k];
+        }
+    int D = 1;
+    for (int d = 2; d <= Mx - mi; d++) {
+        bool all = true;
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            if ((mask >> k) & 1u) all = all && ((idx[k] - mi) % d == 0);
+        if (all) D = d;
+    }
+    int Mi = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        cidx0[k] = ((mask >> k) & 1u) ? (idx[k] - mi) / D : 0;
+        Mi = Mi > cidx0[k] ? Mi : cidx0[k];
+    }
+    float err_o = 3.402823466e+38f;
+    if (Mi == 0) {
+        // quant_single_point_d without USE_RAMPS: index 0, end points 0, out 0
+        float t = 0;
+        if (!alls)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                if ((mask >> i) & 1u)
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) t += (din[i][j] - 0.0f) * (din[i][j] - 0.0f);
+        if (t < err_o) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) idx[k] = 0;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) epo[0][j] = epo[1][j] = 0;
+            err_o = t;
+        }
+        return err_o;
+    }
+    float err_2 = 3.402823466e+38f;
+    uint64_t idx_2 = 0;
+    int epo_2[2][3] = {{0, 0, 0}, {0, 0, 0}};
+    for (int q = 1; q * Mi <= Mi_; q++)
+        for (int p = 0; p <= Mi_ - q * Mi; p++) {
+            // least squares on the rounded cluster means (:2377-2437)
+            float im00 = 0, im01 = 0, im11 = 0, rp[2][3] = {{0, 0, 0}, {0, 0, 0}};
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if ((mask >> k) & 1u) {
+                    const int ck = cidx0[k] * q + p;
+                    // cluster_mean_d_d: the members of this cluster in texel order
+                    float sm[3] = {0, 0, 0};
+                    int cnt = 0;
+#pragma unroll
+                    for (int u = 0; u < 16; ++u)
+                        if (((mask >> u) & 1u) && cidx0[u] == cidx0[k]) {
+                            ++cnt;
+#pragma unroll
+                            for (int j = 0; j < 3; ++j) sm[j] += din[u][j];
+                        }
+                    im00 += (float)((Mi_ - ck) * (Mi_ - ck));
+                    im01 += (float)(ck * (Mi_ - ck));
+                    im11 += (float)(ck * ck);
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) {
+                        const float cc = floorf(sm[j] / (float)cnt + 0.5f);
+                        rp[0][j] += (float)(Mi_ - ck) * cc;
+                        rp[1][j] += (float)ck * cc;
+                    }
+                }
+            const float dd = im00 * im11 - im01 * im01;
+            const float i10 = im00;
+            const float a00 = im11 / dd, a11 = i10 / dd, a01 = -im01 / dd;
+            float epd[2][3][2];
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const float e0 = (a00 * rp[0][j] + a01 * rp[1][j]) * (float)Mi_;
+                const float e1 = (a01 * rp[0][j] + a11 * rp[1][j]) * (float)Mi_;
+                epd[0][j][0] = epd[0][j][1] = e0;
+                epd[1][j][0] = epd[1][j][1] = e1;
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const int lim = (int)(255u - (uint32_t)cvt_i32(epd[i][j][1]));
+                    epd[i][j][1] += (float)(lim < 1 ? lim : 1);
+                }
+            }
+            // the 64-corner walk (:2476-2549): corner s takes, per channel j,
+            // end point 0's candidate (s >> 2j) & 1 and end point 1's (s >> 2j+1) & 1
+            float eq[2][3][2];   // their expanded codes
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) eq[i][j][c] = ep8(cvt_i32(epd[i][j][c]));
+            float err_1 = 3.402823466e+38f;
+            uint64_t idx_1 = 0;
+            int s1 = 0, s = 0;
+            for (int p1 = 0; p1 < 64; p1++) {
+                s ^= p1 & (-p1);
+                float R[3][NCL];
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    const float a = ((s >> (2 * j)) & 1) ? eq[0][j][1] : eq[0][j][0];
+                    const float b = ((s >> (2 * j + 1)) & 1) ? eq[1][j][1] : eq[1][j][0];
+#pragma unroll
+                    for (int c = 0; c < NCL; ++c) R[j][c] = ramp8<CLOG>(a, b, c);
+                }
+                float err_0 = 0;
+                uint64_t idx_0 = 0;
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    if ((mask >> i) & 1u) {
+                        int ci = 0;
+                        float cmin = 3.402823466e+38f;
+#pragma unroll
+                        for (int c = 0; c < NCL; c++) {
+                            const float r0 = R[0][c] - din[i][0], r1 = R[1][c] - din[i][1], r2 = R[2][c] - din[i][2];
+                            float t_ = 0.f;
+                            t_ += r0 * r0;
+                            t_ += r1 * r1;
+                            t_ += r2 * r2;
+                            if (t_ < cmin) {
+                                cmin = t_;
+                                ci = c;
+                            }
+                        }
+                        idx_0 |= (uint64_t)ci << (4 * i);
+                        err_0 += cmin;
+                    }
+                if (err_0 < err_1) {
+                    idx_1 = idx_0;
+                    err_1 = err_0;
+                    s1 = s;
+                }
+            }
+            if (err_1 < err_2) {
+                idx_2 = idx_1;
+                err_2 = err_1;
+#pragma unroll
+                for (int j = 0; j < 3; j++) {
+                    epo_2[0][j] = cvt_i32(epd[0][j][(s1 >> (2 * j)) & 1]);
+                    epo_2[1][j] = cvt_i32(epd[1][j][(s1 >> (2 * j + 1)) & 1]);
+                }
+            }
+        }
+    if (err_2 < err_o) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if ((mask >> k) & 1u) idx[k] = nib(idx_2, k);
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            epo[0][j] = epo_2[0][j];
+            epo[1][j] = epo_2[1][j];
+        }
+        err_o = err_2;
+    }
+    return err_o;
+}
+
+__device__ __forceinline__ float shaker_dispatch(const float din[16][3], uint32_t mask, int idx[16], int epo[2][3])
+{
+    const int n = __popc(mask);
+    if (n >= 8) return shaker_hd<3>(din, mask, n, idx, epo);
+    if (n >= 4) return shaker_hd<2>(din, mask, n, idx, epo);
+    if (n >= 2) return shaker_hd<1>(din, mask, n, idx, epo);
+    return shaker_hd<0>(din, mask, n, idx, epo);
+}
+
+// ---------------------------------------------------------- block loading ---
+
+struct Src {
+    const float *blocks;   // float RGBA blocks (64 per block), or null: the image
+    Geometry g;
+    int force_alpha_one;
+};
+
+// CompressBlock's texel conversion (:1539-1573)
+__device__ __forceinline__ void load_din(const Src &src, uint32_t b, int is_signed, float din[16][3])
+{
+    float blk[64];
+    if (src.blocks) {
+        const float4 *p = reinterpret_cast<const float4 *>(src.blocks + (size_t)b * 64);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float4 v = p[i];
+            blk[i * 4 + 0] = v.x;
+            blk[i * 4 + 1] = v.y;
+            blk[i * 4 + 2] = v.z;
+            blk[i * 4 + 3] = v.w;
+        }
+    } else {
+        uint32_t slice, by, bx;
+        block_coords(src.g, b, slice, by, bx);
+        load_block(src.g, slice, by, bx, src.force_alpha_one != 0, blk);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float v = blk[i * 4 + c];
+            if ((double)v < 0.00001)
+                din[i][c] = is_signed ? (float)-(int)f2h(fabsf(v / 1.0f)) : 0.0f;
+            else
+                din[i][c] = (float)(int)f2h(v / 1.0f);
+        }
+}
+
+__device__ __forceinline__ uint32_t subset_mask(int shape, int sub)
+{
+    if (shape < 0) return sub ? 0u : 0xFFFFu;
+    const uint32_t w = dShape[shape];
+    uint32_t m = 0;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) m |= (((w >> (2 * t)) & 3u) == (uint32_t)sub ? 1u : 0u) << t;
+    return m;
+}
+
+__device__ __forceinline__ float clamp_f16(float v, int is_signed)
+{
+    if (is_signed) {
+        if (v < -kF16Max) return -kF16Max;
+        if (v > kF16Max) return kF16Max;
+    } else {
+        if (v < 0.0) return 0;
+        if (v > kF16Max) return kF16Max;
+    }
+    return v;
+}
+
+// lerpf (:66-81) for denominators 7 and 15
+__device__ __forceinline__ float lerp_pal(float a, float b, int i, int denom)
+{
+    const int w7[8] = {0, 9, 18, 27, 37, 46, 55, 64};
+    const int w15[16] = {0, 4, 9, 13, 17, 21, 26, 30, 34, 38, 43, 47, 51, 55, 60, 64};
+    int wa = 0, wb = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int v = denom == 7 ? (k < 8 ? w7[k] : 0) : w15[k];
+        wa = k == denom - i ? v : wa;
+        wb = k == i ? v : wb;
+    }
+    return (a * (float)wa + b * (float)wb) / 64.0f;
+}
+
+// palitizeEndPointsF (:707-758): region 1 = 16 entries of subset 0, region 2
+// = 8 entries per subset (pal[sub * 8 + i])
+template <int REGION>
+__device__ __forceinline__ void palette(const float fep[12], float pal[16][3])
+{
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            if (REGION == 1)
+                pal[i][c] = lerp_pal(fep[c], fep[3 + c], i, 15);
+            else
+                pal[i][c] = lerp_pal(fep[(i >> 3) * 6 + c], fep[(i >> 3) * 6 + 3 + c], i & 7, 7);
+        }
+}
+
+// CalcShapeError (:783-836): per texel, the palette scan of its subset from
+// entry 0 while the sum of absolute differences does not increase
+template <int REGION>
+__device__ __forceinline__ float shape_error(const float din[16][3], uint32_t m1, const float pal[16][3])
+{
+    constexpr int MAXP = REGION == 1 ? 16 : 8;
+    float total = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const bool sub = REGION == 2 && ((m1 >> i) & 1u);
+        float best = 0.f;
+        bool go = true;
+#pragma unroll
+        for (int j = 0; j < MAXP; j++) {
+            const float p0 = sub ? pal[8 + (j & 7)][0] : pal[j][0], p1 = sub ? pal[8 + (j & 7)][1] : pal[j][1],
+                        p2 = sub ? pal[8 + (j & 7)][2] : pal[j][2];
+            const float er = fabsf(din[i][0] - p0) + fabsf(din[i][1] - p1) + fabsf(din[i][2] - p2);
+            if (j == 0) {
+                best = er;
+            } else if (go && best > 0) {
+                if (er <= best)
+                    best = er;
+                else
+                    go = false;
+            }
+        }
+        total += best;
+    }
+    return total;
+}
+
+// K1: FindBestPattern for (block, pattern)
+__global__ void __launch_bounds__(256) k_bc6h_pattern(Src src, uint32_t first, uint32_t n, int is_signed,
+                                                      PatternState *__restrict__ ws)
+{
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t b = gid / kPatterns;
+    const int pat = (int)(gid % kPatterns);
+    if (b >= n) return;
+    float din[16][3];
+    load_din(src, first + b, is_signed, din);
+    const int shape = pat - 1;
+    const int ns = shape >= 0 ? 2 : 1, ncl = shape >= 0 ? 8 : 16;
+    float dir[3] = {0.f, 0.f, 0.f};
+    float err0 = 0.0f;
+    float ep[2][2][3] = {};
+    int qidx[16];
+    uint64_t idx0 = 0;
+    uint32_t masks[2] = {subset_mask(shape, 0), subset_mask(shape, 1)};
+    for (int s = 0; s < ns; ++s) {
+        err0 += opt_quant_f(din, masks[s], ncl, qidx, dir, ep[s]);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if ((masks[s] >> k) & 1u) idx0 = set_nib(idx0, k, qidx[k]);
+    }
+    PatternState st;
+    st.pad = 0.f;
+    uint64_t idx = idx0;
+    bool shaker = false;
+    int epo[2][2][3] = {};
+    if (shape >= 0) {   // USE_SHAKERHD, quality 1.0 > 0.80 (:960-1025)
+        float err1 = 0.0f;
+        uint64_t idx1 = 0;
+        for (int s = 0; s < 2; ++s) {
+            int tmp[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) tmp[k] = nib(idx0, k);
+            err1 += shaker_dispatch(din, masks[s], tmp, epo[s]);
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if ((masks[s] >> k) & 1u) idx1 = set_nib(idx1, k, tmp[k]);
+        }
+        if (err0 > err1) {
+            shaker = true;
+            idx = idx1;
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                st.fep[(s * 2 + e) * 3 + c] =
+                    clamp_f16(shaker && s < ns ? (float)epo[s][e][c] : ep[s][e][c], is_signed);
+    st.idx = idx;
+    float pal[16][3];
+    if (shape >= 0) {
+        palette<2>(st.fep, pal);
+        st.err = shape_error<2>(din, masks[1], pal);
+    } else {
+        palette<1>(st.fep, pal);
+        st.err = shape_error<1>(din, 0u, pal);
+    }
+    ws[(size_t)b * kPatterns + pat] = st;
+}
+
+// ---------------------------------------------------------- EncodePattern ---
+
+struct ModePart {
+    int nbits, prec[3], transformed, index_prec, mode;
+};
+// ModePartition (amd_bc6h_body.hpp:157-178), modes 1..10
+__constant__ ModePart kMP[11] = {
+    {0, {0, 0, 0}, 0, 0, 0},     {10, {5, 5, 5}, 1, 3, 0x00}, {7, {6, 6, 6}, 1, 3, 0x01}, {11, {5, 4, 4}, 1, 3, 0x02},
+    {11, {4, 5, 4}, 1, 3, 0x06}, {11, {4, 4, 5}, 1, 3, 0x0a}, {9, {5, 5, 5}, 1, 3, 0x0e}, {8, {6, 5, 5}, 1, 3, 0x12},
+    {8, {5, 6, 5}, 1, 3, 0x16},  {8, {5, 5, 6}, 1, 3, 0x1a},  {6, {6, 6, 6}, 0, 3, 0x1e},
+};
+
+__device__ __forceinline__ int maskn(int n) { return (1 << n) - 1; }
+__device__ __forceinline__ int sign_extend(int w, int tbits)
+{
+    return ((w & (1 << (tbits - 1))) ? (int)(~0u << tbits) : 0) | w;
+}
+
+// QuantizeToInt (amd_hdr_encode.cpp:83-115) of (short)(int)v
+__device__ __forceinline__ int quantize_to_int(float v, int prec, int is_signed)
+{
+    const short value = (short)cvt_i32(v);
+    if (prec <= 1) return 0;
+    bool neg = false;
+    const int ivalue = value;
+    if (is_signed) {
+        neg = value < 0;
+        prec--;
+    }
+    int bias = (prec > 10 && prec != 16) ? ((1 << (prec - 11)) - 1) : 0;
+    bias = (prec == 16) ? 15 : bias;
+    const int q = (int)(((long long)ivalue * (1ll << prec) + bias) / (kF16Max + 1));
+    return neg ? -q : q;
+}
+
+__device__ __forceinline__ bool is_overflow(int v, int nbit)
+{
+    return !(v >= -(1 << (nbit - 1)) && v <= (1 << (nbit - 1)) - 1);
+}
+
+// TransformEndPoints (amd_bc6h_body.cpp:598-660), two regions
+__device__ bool transform_ep(const ModePart &mp, const int ie[12], int oe[12])
+{
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        const int p = mp.prec[i], pm = maskn(p);
+        oe[i] = ie[i] & maskn(mp.nbits);
+        if (mp.transformed) {
+#pragma unroll
+            for (int r = 1; r < 4; ++r) {
+                const int d = ie[r * 3 + i] - ie[i];
+                if (is_overflow(d, p)) return false;
+                oe[r * 3 + i] = d & pm;
+            }
+        } else {
+#pragma unroll
+            for (int r = 1; r < 4; ++r) oe[r * 3 + i] = ie[r * 3 + i] & pm;
+        }
+    }
+    return true;
+}
+
+// endpts_fit (:493-507) with decompress_endpts (:458-490)
+__device__ bool endpoints_fit(const ModePart &mp, const int orig[12], const int comp[12], int is_signed)
+{
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        int un[4];
+        if (mp.transformed) {
+            un[0] = is_signed ? sign_extend(comp[i], mp.index_prec) : comp[i];
+#pragma unroll
+            for (int r = 1; r < 4; ++r) {
+                const int t = (sign_extend(comp[r * 3 + i], mp.prec[i]) + comp[i]) & maskn(mp.nbits);
+                un[r] = is_signed ? sign_extend(t, mp.nbits) : t;
+            }
+        } else {
+            un[0] = is_signed ? sign_extend(comp[i], mp.nbits) : comp[i];
+#pragma unroll
+            for (int r = 1; r < 4; ++r) un[r] = is_signed ? sign_extend(comp[r * 3 + i], mp.prec[i]) : comp[r * 3 + i];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ok = ok && orig[r * 3 + i] == un[r];
+    }
+    return ok;
+}
+
+// Unquantize (:117-150) + finish_unquantizeF16 (:1039-1049), unsigned
+__device__ __forceinline__ float unq_f16(int comp, int bits)
+{
+    int unq;
+    if (bits >= 15)
+        unq = comp;
+    else if (comp == 0)
+        unq = 0;
+    else if (comp == ((1 << bits) - 1))
+        unq = 0xFFFF;
+    else
+        unq = ((comp << 16) + 0x8000) >> bits;
+    return (float)((unq * 31) >> 6);
+}
+
+// decompress_endpoints2 (:1134-1252), the unsigned branches (issigned is never set)
+__device__ void decode_ep2(const ModePart &mp, const int oe[12], float out[12])
+{
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        int o[4];
+        o[0] = oe[i];
+#pragma unroll
+        for (int r = 1; r < 4; ++r)
+            o[r] = mp.transformed ? (sign_extend(oe[r * 3 + i], mp.prec[i]) + oe[i]) & maskn(mp.nbits) : oe[r * 3 + i];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[r * 3 + i] = unq_f16(o[r], mp.nbits);
+    }
+}
+
+// SwapIndices (:555-581): subset 0's anchor is texel 0, subset 1's dAnchor[shape]
+__device__ void swap_indices(int ie[12], uint64_t &idx, int shape, uint32_t m1)
+{
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const int at = s ? (int)dAnchor[shape] : 0;
+        if (nib(idx, at) & 4) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const int t = ie[s * 6 + c];
+                ie[s * 6 + c] = ie[s * 6 + 3 + c];
+                ie[s * 6 + 3 + c] = t;
+            }
+            const uint32_t ms = s ? m1 : (~m1 & 0xFFFFu);
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if ((ms >> k) & 1u) idx = set_nib(idx, k, 7 - nib(idx, k));
+        }
+    }
+}
+
+// SaveDataBlock field layout (amd_bc6h_body.cpp:132-364): per mode, (first
+// bit, bits, field, shift); fields rw gw bw rx gx bx ry gy by rz gz bz, 12 = mode
+struct BitField {
+    uint8_t start, bits, field, shift;
+};
+enum { RW, GW, BW, RX, GX, BX, RY, GY, BY, RZ, GZ, BZ, MV };
+__constant__ BitField kLayout[11][24] = {
+    {{0, 0, 0, 0}},
+    {{0, 2, MV, 0},   {2, 1, GY, 4},   {3, 1, BY, 4},   {4, 1, BZ, 4},   {5, 10, RW, 0}, {15, 10, GW, 0},
+     {25, 10, BW, 0}, {35, 5, RX, 0},  {40, 1, GZ, 4},  {41, 4, GY, 0},  {45, 5, GX, 0}, {50, 1, BZ, 0},
+     {51, 4, GZ, 0},  {55, 5, BX, 0},  {60, 1, BZ, 1},  {61, 4, BY, 0},  {65, 5, RY, 0}, {70, 1, BZ, 2},
+     {71, 5, RZ, 0},  {76, 1, BZ, 3},  {0, 0, 0, 0}},
+    {{0, 2, MV, 0},   {2, 1, GY, 5},   {3, 1, GZ, 4},   {4, 1, GZ, 5},   {5, 7, RW, 0},  {12, 1, BZ, 0},
+     {13, 1, BZ, 1},  {14, 1, BY, 4},  {15, 7, GW, 0},  {22, 1, BY, 5},  {23, 1, BZ, 2}, {24, 1, GY, 4},
+     {25, 7, BW, 0},  {32, 1, BZ, 3},  {33, 1, BZ, 5},  {34, 1, BZ, 4},  {35, 6, RX, 0}, {41, 4, GY, 0},
+     {45, 6, GX, 0},  {51, 4, GZ, 0},  {55, 6, BX, 0},  {61, 4, BY, 0},  {65, 6, RY, 0}, {71, 6, RZ, 0}},
+    {{0, 5, MV, 0},   {5, 10, RW, 0},  {15, 10, GW, 0}, {25, 10, BW, 0}, {35, 5, RX, 0}, {40, 1, RW, 10},
+     {41, 4, GY, 0},  {45, 4, GX, 0},  {49, 1, GW, 10}, {50, 1, BZ, 0},  {51, 4, GZ, 0}, {55, 4, BX, 0},
+     {59, 1, BW, 10}, {60, 1, BZ, 1},  {61, 4, BY, 0},  {65, 5, RY, 0},  {70, 1, BZ, 2}, {71, 5, RZ, 0},
+     {76, 1, BZ, 3},  {0, 0, 0, 0}},
+    {{0, 5, MV, 0},   {5, 10, RW, 0},  {15, 10, GW, 0}, {25, 10, BW, 0}, {35, 4, RX, 0}, {39, 1, RW, 10},
+     {40, 1, GZ, 4},  {41, 4, GY, 0},  {45, 5, GX, 0},  {50, 1, GW, 10}, {51, 4, GZ, 0}, {55, 4, BX, 0},
+     {59, 1, BW, 10}, {60, 1, BZ, 1},  {61, 4, BY, 0},  {65, 4, RY, 0},  {69, 1, BZ, 0}, {70, 1, BZ, 2},
+     {71, 4, RZ, 0},  {75, 1, GY, 4},  {76, 1, BZ, 3},  {0, 0, 0, 0}},
+    {{0, 5, MV, 0},   {5, 10, RW, 0},  {15, 10, GW, 0}, {25, 10, BW, 0}, {35, 4, RX, 0}, {39, 1, RW, 10},
+     {40, 1, BY, 4},  {41, 4, GY, 0},  {45, 4, GX, 0},  {49, 1, GW, 10}, {50, 1, BZ, 0}, {51, 4, GZ, 0},
+     {55, 5, BX, 0},  {60, 1, BW, 10}, {61, 4, BY, 0},  {65, 4, RY, 0},  {69, 1, BZ, 1}, {70, 1, BZ, 2},
+     {71, 4, RZ, 0},  {75, 1, BZ, 4},  {76, 1, BZ, 3},  {0, 0, 0, 0}},
+    {{0, 5, MV, 0},   {5, 9, RW, 0},   {14, 1, BY, 4},  {15, 9, GW, 0},  {24, 1, GY, 4}, {25, 9, BW, 0},
+     {34, 1, BZ, 4},  {35, 5, RX, 0},  {40, 1, GZ, 4},  {41, 4, GY, 0},  {45, 5, GX, 0}, {50, 1, BZ, 0},
+     {51, 4, GZ, 0},  {55, 5, BX, 0},  {60, 1, BZ, 1},  {61, 4, BY, 0},  {65, 5, RY, 0}, {70, 1, BZ, 2},
+     {71, 5, RZ, 0},  {76, 1, BZ, 3},  {0, 0, 0, 0}},
+    {{0, 5, MV, 0},   {5, 8, RW, 0},   {13, 1, GZ, 4},  {14, 1, BY, 4},  {15, 8, GW, 0}, {23, 1, BZ, 2},
+     {24, 1, GY, 4},  {25, 8, BW, 0},  {33, 1, BZ, 3},  {34, 1, BZ, 4},  {35, 6, RX, 0}, {41, 4, GY, 0},
+     {45, 5, GX, 0},  {50, 1, BZ, 0},  {51, 4, GZ, 0},  {55, 5, BX, 0},  {60, 1, BZ, 1}, {61, 4, BY, 0},
+     {65, 6, RY, 0},  {71, 6, RZ, 0},  {0, 0, 0, 0}},
+    {{0, 5, MV, 0},   {5, 8, RW, 0},   {13, 1, BZ, 0},  {14, 1, BY, 4},  {15, 8, GW, 0}, {23, 1, GY, 5},
+     {24, 1, GY, 4},  {25, 8, BW, 0},  {33, 1, GZ, 5},  {34, 1, BZ, 4},  {35, 5, RX, 0}, {40, 1, GZ, 4},
+     {41, 4, GY, 0},  {45, 6, GX, 0},  {51, 4, GZ, 0},  {55, 5, BX, 0},  {60, 1, BZ, 1}, {61, 4, BY, 0},
+     {65, 5, RY, 0},  {70, 1, BZ, 2},  {71, 5, RZ, 0},  {76, 1, BZ, 3},  {0, 0, 0, 0}},
+    {{0, 5, MV, 0},   {5, 8, RW, 0},   {13, 1, BZ, 1},  {14, 1, BY, 4},  {15, 8, GW, 0}, {23, 1, BY, 5},
+     {24, 1, GY, 4},  {25, 8, BW, 0},  {33, 1, BZ, 5},  {34, 1, BZ, 4},  {35, 5, RX, 0}, {40, 1, GZ, 4},
+     {41, 4, GY, 0},  {45, 5, GX, 0},  {50, 1, BZ, 0},  {51, 4, GZ, 0},  {55, 6, BX, 0}, {61, 4, BY, 0},
+     {65, 5, RY, 0},  {70, 1, BZ, 2},  {71, 5, RZ, 0},  {76, 1, BZ, 3},  {0, 0, 0, 0}},
+    {{0, 5, MV, 0},   {5, 6, RW, 0},   {11, 1, GZ, 4},  {12, 1, BZ, 0},  {13, 1, BZ, 1}, {14, 1, BY, 4},
+     {15, 6, GW, 0},  {21, 1, GY, 5},  {22, 1, BY, 5},  {23, 1, BZ, 2},  {24, 1, GY, 4}, {25, 6, BW, 0},
+     {31, 1, GZ, 5},  {32, 1, BZ, 3},  {33, 1, BZ, 5},  {34, 1, BZ, 4},  {35, 6, RX, 0}, {41, 4, GY, 0},
+     {45, 6, GX, 0},  {51, 4, GZ, 0},  {55, 6, BX, 0},  {61, 4, BY, 0},  {65, 6, RY, 0}, {71, 6, RZ, 0}},
+};
+
+// BitHeader::setvalue (:88-100) into a 128-bit block held as 4 words
+__device__ __forceinline__ void set_bits(uint32_t w[4], int start, int bits, int value, int shift)
+{
+    for (int k = 0; k < bits; ++k) {
+        const int pos = start + k;
+        const uint32_t bit = ((uint32_t)value >> (shift + k)) & 1u;
+        const int wi = pos >> 5, bi = pos & 31;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (q == wi) w[q] = (w[q] & ~(1u << bi)) | (bit << bi);
+    }
+}
+
+__device__ void save_block(int mode, int shape, const int oe[12], uint64_t idx, uint32_t m1, uint4 *out)
+{
+    // the reference's field names: w = [0][0], x = [0][1], y = [1][0], z = [1][1]
+    int f[13];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        f[RW + c] = oe[c];
+        f[RX + c] = oe[3 + c];
+        f[RY + c] = oe[6 + c];
+        f[RZ + c] = oe[9 + c];
+    }
+    f[MV] = kMP[mode].mode;
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 24; ++k) {
+        const BitField bf = kLayout[mode][k];
+        if (!bf.bits) break;
+        int v = 0;
+#pragma unroll
+        for (int q = 0; q < 13; ++q) v = q == bf.field ? f[q] : v;
+        set_bits(w, bf.start, bf.bits, v, bf.shift);
+    }
+    set_bits(w, 77, 5, shape, 0);
+    const int anc = dAnchor[shape];
+    int start = 82, nb = 2;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (i) {
+            start += nb;
+            nb = anc == i ? 2 : 3;
+        }
+        set_bits(w, start, nb, nib(idx, i), 0);
+    }
+    (void)m1;
+    *out = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// ReIndexShapef (:838-902): each texel's nearest palette entry of its subset
+// (first strictly smaller sum of absolute differences)
+__device__ __forceinline__ uint64_t reindex(const float din[16][3], const float pal[16][3], uint32_t m1)
+{
+    uint64_t idx = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const bool sub = (m1 >> i) & 1u;
+        float best = 3.402823466e+38f;
+        int bi = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const float p0 = sub ? pal[8 + j][0] : pal[j][0], p1 = sub ? pal[8 + j][1] : pal[j][1],
+                        p2 = sub ? pal[8 + j][2] : pal[j][2];
+            const float e = fabsf(din[i][0] - p0) + fabsf(din[i][1] - p1) + fabsf(din[i][2] - p2);
+            if (e < best) {
+                best = e;
+                bi = j;
+            }
+        }
+        idx |= (uint64_t)bi << (4 * i);
+    }
+    return idx;
+}
+
+__constant__ uint32_t kRedBlock[4] = {0x00007bc2u, 0x00000000u, 0x0003e000u, 0x00000000u};
+
+// K2: pattern selection (:1593-1632), EncodePattern (:1351-1488), SaveDataBlock
+__global__ void __launch_bounds__(256) k_bc6h_encode(Src src, uint32_t first, uint32_t n, int is_signed,
+                                                     const PatternState *__restrict__ ws, uint4 *__restrict__ dst,
+                                                     double *__restrict__ err_out)
+{
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= n) return;
+    const PatternState *pst = ws + (size_t)b * kPatterns;
+    float best_err = pst[0].err;
+    int best = -1;
+    for (int s = 0; s < 32; ++s) {
+        const float e = pst[1 + s].err;
+        if (e < best_err) {
+            best_err = e;
+            best = s;
+        }
+    }
+    const int shape = best >= 0 ? best : 31;   // nothing restored when the one-region pattern wins
+    const PatternState st = pst[1 + shape];
+    float din[16][3];
+    load_din(src, first + b, is_signed, din);
+    const uint32_t m1 = subset_mask(shape, 1);
+    float error = best_err, best_e = 3.402823466e+38f;
+    int best_fit = 0, numfits = 0;
+    int best_q[12];
+    uint64_t best_idx = 0;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) best_q[k] = 0;
+    for (int m = 1; m <= 10; ++m) {
+        const ModePart mp = kMP[m];
+        int ie[12], oe[12];
+        uint64_t idx = st.idx;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) ie[k] = quantize_to_int(st.fep[k], mp.nbits, is_signed);
+        swap_indices(ie, idx, shape, m1);
+        if (!transform_ep(mp, ie, oe)) continue;
+        if (!endpoints_fit(mp, ie, oe, is_signed)) continue;
+        numfits++;
+        float dec[12];
+        decode_ep2(mp, oe, dec);
+        float pal[16][3];
+        palette<2>(dec, pal);
+        if (!is_signed) idx = reindex(din, pal, m1);
+        const float e = shape_error<2>(din, m1, pal);
+        if (e < best_e) {
+            bool tf = true;
+            if (!is_signed) {
+#pragma unroll
+                for (int k = 0; k < 12; ++k) ie[k] = quantize_to_int(dec[k], mp.nbits, 0);
+                swap_indices(ie, idx, shape, m1);
+                tf = transform_ep(mp, ie, oe);
+            }
+            if (tf) {
+                best_fit = m;
+                best_e = e;
+                error = e;
+#pragma unroll
+                for (int k = 0; k < 12; ++k) best_q[k] = oe[k];
+                best_idx = idx;
+            }
+        }
+    }
+    if (numfits > 0 && best_fit > 0) {
+        save_block(best_fit, shape, best_q, best_idx, m1, dst + first + b);
+    } else {
+        dst[first + b] = make_uint4(kRedBlock[0], kRedBlock[1], kRedBlock[2], kRedBlock[3]);
+    }
+    if (err_out) err_out[first + b] = (double)error;
+}
+
+// ------------------------------------------------------------------ host ---
+
+constexpr uint32_t kChunk = 1u << 16;
+
+static hipError_t upload_tables()
+{
+    static bool done = false;   // guarded by the caller's lock
+    static int dev_done = -1;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (done && dev_done == dev) return hipSuccess;
+    uint32_t shp[32];
+    uint8_t anc[32];
+    for (int s = 0; s < 32; ++s) {
+        shp[s] = kBc7Shape2[s];
+        anc[s] = kBc7Anchor2[s];
+    }
+    e = hipMemcpyToSymbol(HIP_SYMBOL(dShape), shp, sizeof(shp));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dAnchor), anc, sizeof(anc));
+    if (e == hipSuccess) {
+        done = true;
+        dev_done = dev;
+    }
+    return e;
+}
+
+}  // namespace bc6h
+
+static std::mutex g_bc6h_lock;
+
+// n blocks from float RGBA blocks (blocks != null) or from the image g, in
+// passes of kChunk blocks with a stream-ordered pattern workspace
+static hipError_t bc6h_run(const float *blocks, const Geometry *g, uint32_t n, int is_signed, int force_alpha_one,
+                           void *dst, double *err, hipStream_t s)
+{
+    using namespace bc6h;
+    {
+        std::lock_guard<std::mutex> lk(g_bc6h_lock);
+        const hipError_t e = upload_tables();
+        if (e != hipSuccess) return e;
+    }
+    const uint32_t chunk = n < kChunk ? n : kChunk;
+    PatternState *ws = nullptr;
+    hipError_t e = hipMallocAsync((void **)&ws, (size_t)chunk * kPatterns * sizeof(PatternState), s);
+    if (e != hipSuccess) return e;
+    Src src;
+    src.blocks = blocks;
+    if (g) src.g = *g;
+    src.force_alpha_one = force_alpha_one;
+    for (uint32_t first = 0; first < n; first += chunk) {
+        const uint32_t m = (n - first) < chunk ? (n - first) : chunk;
+        const uint64_t nl = (uint64_t)m * kPatterns;
+        hipLaunchKernelGGL(k_bc6h_pattern, dim3((uint32_t)((nl + 255) / 256)), dim3(256), 0, s, src, first, m,
+                           is_signed, ws);
+        hipLaunchKernelGGL(k_bc6h_encode, dim3((m + 255) / 256), dim3(256), 0, s, src, first, m, is_signed,
+                           (const PatternState *)ws, (uint4 *)dst, err);
+        e = hipGetLastError();
+        if (e != hipSuccess) break;
+    }
+    const hipError_t ef = hipFreeAsync(ws, s);
+    return e != hipSuccess ? e : ef;
+}
+
+hipError_t launch_bc6h_blocks(const float *blocks, uint32_t n, int is_signed, void *dst, double *err, hipStream_t s)
+{
+    return bc6h_run(blocks, nullptr, n, is_signed, 0, dst, err, s);
+}
+
+hipError_t launch_bc6h_image(const Geometry &g, int is_signed, int force_alpha_one, void *dst, double *err,
+                             hipStream_t s)
+{
+    return bc6h_run(nullptr, &g, g.total, is_signed, force_alpha_one, dst, err, s);
+}
+
+}  // namespace gic

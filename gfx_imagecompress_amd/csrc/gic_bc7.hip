@@ -1279,7 +1279,12 @@ struct Params {
     double bound_sse;
     int skip_done;
     int probe;   // bounded-exit probe: modes legal without the colour restriction (meta.pvalid)
+    // workspace slot b holds output block list[b] (a compacted list of the
+    // blocks an earlier stage left unfinished), or first + b when list is null
+    const uint32_t *list;
 };
+
+__device__ __forceinline__ uint32_t out_block(const Params &p, uint32_t b) { return p.list ? p.list[b] : p.first + b; }
 
 // BlockMeta.flags bit 2: the block met the error threshold in an earlier
 // stage (CompressBlock's mode-loop exit, :1440-1446)
@@ -1379,7 +1384,7 @@ __global__ void __launch_bounds__(256) k_prep_image(Geometry g, Params p, Worksp
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= p.n) return;
     uint32_t slice, by, bx;
-    block_coords(g, p.first + b, slice, by, bx);
+    block_coords(g, out_block(p, b), slice, by, bx);
     float blk[64];
     load_block(g, slice, by, bx, p.force_alpha_one != 0, blk);
     prep_block(blk, p, ws.tex + (size_t)b * 64, ws.meta[b]);
@@ -1390,7 +1395,8 @@ __global__ void __launch_bounds__(256) k_prep_f32(const float *__restrict__ bloc
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= p.n) return;
     float blk[64];
-    for (int i = 0; i < 64; ++i) blk[i] = blocks[(size_t)(p.first + b) * 64 + i];
+    const size_t o = (size_t)out_block(p, b) * 64;
+    for (int i = 0; i < 64; ++i) blk[i] = blocks[o + i];
     prep_block(blk, p, ws.tex + (size_t)b * 64, ws.meta[b]);
 }
 
@@ -2123,7 +2129,7 @@ __global__ void __launch_bounds__(256) k_select(Params p, Workspace ws, uint4 *_
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= p.n) return;
     BlockMeta meta = ws.meta[b];
-    const uint32_t out_id = p.first + b;
+    const uint32_t out_id = out_block(p, b);
     if (meta.flags & 1u) {
         if (k1 == 8) {
             dst[out_id] = make_uint4(0, 0, 0, 0);
@@ -2251,9 +2257,31 @@ __global__ void __launch_bounds__(256) k_bound(Params p, Workspace ws, uint4 *__
     const uint4 v = ws.best_blk[b];
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     if (!(decoded_sse(w, ws.tex + (size_t)b * 64) <= p.bound_sse)) return;
-    dst[p.first + b] = v;
-    if (err_out) err_out[p.first + b] = e;
+    const uint32_t o = out_block(p, b);
+    dst[o] = v;
+    if (err_out) err_out[o] = e;
     ws.meta[b].flags = meta.flags | 4u;
+}
+
+// Stream compaction between bounded-exit stages: the output ids of the
+// chunk's blocks that no stage has finished yet (flag bit 2 clear) are
+// appended to `out` (one atomic per wave; the order of the list does not
+// matter, every block writes its own output slot), so that the next stage's
+// launches are sized by the survivors instead of carrying a dead wave per
+// finished block through every kernel of the full search.
+__global__ void __launch_bounds__(256) k_compact(Params p, Workspace ws, uint32_t *__restrict__ out,
+                                                 uint32_t *__restrict__ count)
+{
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool keep = b < p.n && !(ws.meta[b].flags & 4u);
+    const uint64_t m = __ballot(keep);
+    if (!m) return;
+    const int lane = (int)__lane_id();
+    const int leader = __builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, leader);
+    if (keep) out[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = out_block(p, b);
 }
 
 // ----------------------------------------------------------------- host ---
@@ -2436,7 +2464,38 @@ struct DeviceState {
     hipStream_t lane[2] = {nullptr, nullptr};
     hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
     TraceTab trace{nullptr, nullptr};   // optQuantTrace_d tables, built on first use (performance < 1)
+    // bounded exit: ping-pong survivor lists (output block ids) and per-stage counters
+    uint32_t *list[2] = {nullptr, nullptr};
+    uint32_t list_cap = 0;
+    uint32_t *count = nullptr;   // [4]
 };
+
+// Caller holds g_state_lock.  The lists are replaced only after both lanes
+// drained (earlier calls may still read them).
+static hipError_t get_lists(DeviceState &st, uint32_t total)
+{
+    hipError_t e = hipSuccess;
+    if (!st.count) {
+        e = hipMalloc(&st.count, 4 * sizeof(uint32_t));
+        if (e != hipSuccess) return e;
+    }
+    if (st.list_cap >= total) return hipSuccess;
+    for (int k = 0; k < 2; ++k) {
+        if (st.lane[k]) e = hipStreamSynchronize(st.lane[k]);
+        if (e != hipSuccess) return e;
+    }
+    for (int k = 0; k < 2; ++k) {
+        (void)hipFree(st.list[k]);
+        st.list[k] = nullptr;
+    }
+    st.list_cap = 0;
+    for (int k = 0; k < 2; ++k) {
+        e = hipMalloc(&st.list[k], (size_t)total * sizeof(uint32_t));
+        if (e != hipSuccess) return e;
+    }
+    st.list_cap = total;
+    return hipSuccess;
+}
 
 // Caller holds g_state_lock.
 static hipError_t get_trace(DeviceState &st)
@@ -2632,6 +2691,43 @@ static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, h
 #endif
 constexpr uint32_t kChunk = GIC_BC7_CHUNK;   // blocks per pipeline pass (~1.1 GB workspace per set at 65536)
 
+// BC7BlockEncoder constructor (amd_bc7_body.hpp:94-149): the quality- and
+// performance-derived settings of every pass
+static void base_params(const gic_options &o, const DeviceState &st, double perf, Params &p)
+{
+    p.mode_mask = o.bc7_mode_mask;
+    p.colour_restrict = o.colour_restrict;
+    p.alpha_restrict = o.alpha_restrict;
+    p.force_alpha_one = o.force_alpha_one;
+    const double q = o.bc7_quality;
+    p.quality = q < 1.0 ? (q > 0.0 ? q : 0.0) : 1.0;
+    if (p.quality < 0.5) {
+        p.shake_thr = 0.;
+        p.err_thr = 256. * (1.0 - ((p.quality * 2.0) / 0.5));
+        p.part_search = (1.0 / 16.0) > ((p.quality * 2.0) / 0.5) ? (1.0 / 16.0) : ((p.quality * 2.0) / 0.5);
+    } else if (p.quality < 0.7) {
+        p.shake_thr = 255 * (p.quality / 10);
+        p.err_thr = 256. * (1.0 - (p.quality / 0.5));
+        p.part_search = (1.0 / 16.0) > (p.quality / 0.5) ? (1.0 / 16.0) : (p.quality / 0.5);
+    } else {
+        p.shake_thr = 255 * p.quality;
+        p.err_thr = 0;
+        p.part_search = 1.0;
+    }
+    p.quant_thr = 255 * perf;
+    p.trace = st.trace;
+    p.att = host_attempts(p, o.bc7_shake_ranks);
+    p.decode_select = o.bc7_shake_ranks > 0 && !(p.err_thr > 0);
+    p.dual_cap = 2 * (int)o.bc7_shake_ranks;
+    p.bound_sse = 0.0;
+    p.skip_done = 0;
+    p.probe = 0;
+    p.stage_mask = 0xFFu;
+    p.list = nullptr;
+    p.first = 0;
+    p.n = 0;
+}
+
 static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t total, const gic_options &o, void *dst,
                              double *err, hipStream_t s)
 {
@@ -2655,94 +2751,99 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
         e = get_trace(*st);
         if (e != hipSuccess) return e;
     }
+    Params base;
+    base_params(o, *st, perf, base);
+    // err_thr > 0 (quality < 0.25): CompressBlock stops visiting modes once a
+    // block's best error is within the threshold, so the modes run one stage
+    // at a time in visit order and finished blocks drop out of later stages.
+    const bool staged = base.err_thr > 0;
+    const bool bounded = o.bc7_mse_bound > 0.f && !staged;
+    const int order[8] = {6, 4, 3, 1, 2, 0, 7, 5};
+    const uint32_t valid_modes = o.bc7_mode_mask == 0 ? 0xCFu : o.bc7_mode_mask;
+    if (bounded) {
+        e = get_lists(*st, total);
+        if (e != hipSuccess) return e;
+        e = hipMemsetAsync(st->count, 0, 4 * sizeof(uint32_t), s);
+        if (e != hipSuccess) return e;
+    }
     e = hipEventRecord(st->ev_fork, s);   // fork: the lanes start after the caller's prior work
     for (int k = 0; k < nsets && e == hipSuccess; ++k) e = hipStreamWaitEvent(st->lane[k], st->ev_fork, 0);
     if (e != hipSuccess) return e;
     const hipStream_t caller = s;
+    const uint32_t wg = 256;
+    // Stages: without the bounded exit one (the search); with it the probes
+    // (modes 6, 3, then 1 -- visit positions 0, 2, 3 -- each with two
+    // partitions shaken and the decode-aware choice; k_bound makes a block
+    // final when its probe block decodes within the bound), then the full
+    // search over the blocks no probe finished.  Between stages the
+    // unfinished blocks are compacted into a list (k_compact) and the next
+    // stage runs over that list in dense chunks.  The probes may use mode 6
+    // on opaque blocks, which the reference's colour restriction leaves out
+    // of its own search: any BC7 block within the bound meets the contract.
+    int stages[4], nstages = 0;
+    if (bounded)
+        for (int k : {0, 2, 3})
+            if (valid_modes & (1u << order[k])) stages[nstages++] = k;
+    stages[nstages++] = -1;   // the search itself
+    const uint32_t *cur = nullptr;
+    uint32_t cur_n = total;
     uint32_t ci = 0;
-    for (uint32_t first = 0; first < total; first += chunk, ++ci) {
-        const Workspace &ws = st->ws[nsets > 1 ? (ci & 1) : 0];
-        s = st->lane[nsets > 1 ? (ci & 1) : 0];
-        Params p;
-        p.mode_mask = o.bc7_mode_mask;
-        p.colour_restrict = o.colour_restrict;
-        p.alpha_restrict = o.alpha_restrict;
-        p.force_alpha_one = o.force_alpha_one;
-        p.first = first;
-        p.n = (total - first) < chunk ? (total - first) : chunk;
-        // BC7BlockEncoder constructor (amd_bc7_body.hpp:94-149)
-        const double q = o.bc7_quality;
-        p.quality = q < 1.0 ? (q > 0.0 ? q : 0.0) : 1.0;
-        if (p.quality < 0.5) {
-            p.shake_thr = 0.;
-            p.err_thr = 256. * (1.0 - ((p.quality * 2.0) / 0.5));
-            p.part_search = (1.0 / 16.0) > ((p.quality * 2.0) / 0.5) ? (1.0 / 16.0) : ((p.quality * 2.0) / 0.5);
-        } else if (p.quality < 0.7) {
-            p.shake_thr = 255 * (p.quality / 10);
-            p.err_thr = 256. * (1.0 - (p.quality / 0.5));
-            p.part_search = (1.0 / 16.0) > (p.quality / 0.5) ? (1.0 / 16.0) : (p.quality / 0.5);
-        } else {
-            p.shake_thr = 255 * p.quality;
-            p.err_thr = 0;
-            p.part_search = 1.0;
-        }
-        p.quant_thr = 255 * perf;
-        p.trace = st->trace;
-        p.att = host_attempts(p, o.bc7_shake_ranks);
-        p.decode_select = o.bc7_shake_ranks > 0 && !(p.err_thr > 0);
-        p.dual_cap = 2 * (int)o.bc7_shake_ranks;
-        p.bound_sse = 0.0;
-        p.skip_done = 0;
-        p.probe = 0;
-        const uint32_t wg = 256;
-        if (g)
-            hipLaunchKernelGGL(k_prep_image, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, *g, p, ws);
-        else
-            hipLaunchKernelGGL(k_prep_f32, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, blocks, p, ws);
-        // err_thr > 0 (quality < 0.25): CompressBlock stops visiting modes once a
-        // block's best error is within the threshold, so the modes run one stage
-        // at a time in visit order and finished blocks drop out of later stages.
-        const bool staged = p.err_thr > 0;
-        const int order[8] = {6, 4, 3, 1, 2, 0, 7, 5};
-        const uint32_t valid_modes = o.bc7_mode_mask == 0 ? 0xCFu : o.bc7_mode_mask;
-        if (o.bc7_mse_bound > 0.f && !staged) {
-            // bounded exit: probe modes 6, 3, then 1 (visit positions 0, 2, 3)
-            // with two partitions shaken; blocks within the bound drop out of
-            // every later launch (mode_active), the rest run the full search
-            // below.  The probes may use mode 6 on opaque blocks, which the
-            // reference's colour restriction leaves out of its own search: any
-            // BC7 block within the bound meets the contract.  On G1, mode 6 is
-            // the cheapest probe (a single subset) and already brings 84 % of
-            // blocks within MSE 0.5.
-            Params pp = p;
-            pp.att = host_attempts(pp, 2);
-            pp.decode_select = 1;
-            pp.dual_cap = 4;
-            pp.bound_sse = 64.0 * (double)o.bc7_mse_bound;
-            pp.probe = 1;
-            for (int k : {0, 2, 3}) {
-                pp.stage_mask = 1u << order[k];
-                if (!(valid_modes & pp.stage_mask)) continue;
+    for (int si = 0; si < nstages && cur_n; ++si) {
+        const int pk = stages[si];
+        const bool last_stage = si == nstages - 1;
+        uint32_t *out = bounded ? st->list[si & 1] : nullptr;
+        for (uint32_t first = 0; first < cur_n; first += chunk, ++ci) {
+            const Workspace &ws = st->ws[nsets > 1 ? (ci & 1) : 0];
+            s = st->lane[nsets > 1 ? (ci & 1) : 0];
+            Params p = base;
+            p.first = first;
+            p.n = (cur_n - first) < chunk ? (cur_n - first) : chunk;
+            p.list = cur ? cur + first : nullptr;
+            if (g)
+                hipLaunchKernelGGL(k_prep_image, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, *g, p, ws);
+            else
+                hipLaunchKernelGGL(k_prep_f32, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, blocks, p, ws);
+            if (pk >= 0) {
+                Params pp = p;
+                pp.att = host_attempts(pp, 2);
+                pp.decode_select = 1;
+                pp.dual_cap = 4;
+                pp.bound_sse = 64.0 * (double)o.bc7_mse_bound;
+                pp.probe = 1;
+                pp.stage_mask = 1u << order[pk];
                 run_modes(pp, ws, st->sp, s, g != nullptr);
                 hipLaunchKernelGGL(k_select, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, pp, ws, (uint4 *)dst, err,
-                                   k, k + 1, 0);
+                                   pk, pk + 1, 0);
                 hipLaunchKernelGGL(k_bound, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, pp, ws, (uint4 *)dst, err);
+                hipLaunchKernelGGL(k_compact, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, pp, ws, out,
+                                   st->count + si);
+            } else {
+                int resume = 0;
+                for (int k = 0; k < (staged ? 8 : 1); ++k) {
+                    p.stage_mask = staged ? (1u << order[k]) : 0xFFu;
+                    const bool last = !staged || k == 7;
+                    const bool skip = staged && !(valid_modes & p.stage_mask);
+                    if (skip && !last) continue;
+                    if (!skip) run_modes(p, ws, st->sp, s, g != nullptr);
+                    hipLaunchKernelGGL(k_select, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, p, ws, (uint4 *)dst, err,
+                                       staged ? k : 0, staged ? k + 1 : 8, resume);
+                    resume = 1;
+                }
             }
-            p.skip_done = 1;
+            e = hipGetLastError();
+            if (e != hipSuccess) return e;
         }
-        int resume = 0;
-        for (int k = 0; k < (staged ? 8 : 1); ++k) {
-            p.stage_mask = staged ? (1u << order[k]) : 0xFFu;
-            const bool last = !staged || k == 7;
-            const bool skip = staged && !(valid_modes & p.stage_mask);
-            if (skip && !last) continue;
-            if (!skip) run_modes(p, ws, st->sp, s, g != nullptr);
-            hipLaunchKernelGGL(k_select, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, p, ws, (uint4 *)dst, err,
-                               staged ? k : 0, staged ? k + 1 : 8, resume);
-            resume = 1;
+        if (!last_stage) {
+            // the survivor count sizes the next stage's passes (a host round
+            // trip per stage; the lanes are drained anyway)
+            for (int k = 0; k < nsets && e == hipSuccess; ++k) e = hipStreamSynchronize(st->lane[k]);
+            uint32_t n_next = 0;
+            if (e == hipSuccess) e = hipMemcpy(&n_next, st->count + si, sizeof(uint32_t), hipMemcpyDeviceToHost);
+            if (e != hipSuccess) return e;
+            if (n_next > cur_n) return hipErrorUnknown;   // cannot happen: a stage only removes blocks
+            cur = out;
+            cur_n = n_next;
         }
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
     }
     {   // join: the caller's stream waits for the lanes
         for (int k = 0; k < nsets && e == hipSuccess; ++k) {

@@ -125,3 +125,27 @@ def reference_pattern_rgb(width: int, height: int, punch_through: bool = False, 
         a = (x.astype(np.float32) / np.float32(width))
         img[..., 3] = np.clip(np.round(a * 255.0), 0, 255).astype(np.uint8)
     return img
+
+
+def hdr_rgba(width: int, height: int, seed: int = 1, signed: bool = False) -> np.ndarray:
+    """HDR float32 RGBA (H, W, 4) for BC6H: an exponential ramp over 12 stops
+    (2^-8 .. 2^4) times a smooth hue, with 3 % multiplicative noise and a few
+    bright highlights; signed = values in [-range, range] (sign from a hash)."""
+    y, x = np.mgrid[0:height, 0:width].astype(np.float64)
+    u = x / max(width - 1, 1)
+    v = y / max(height - 1, 1)
+    lum = np.exp2(-8.0 + 12.0 * u)
+    idx = np.arange(width * height, dtype=np.uint64).reshape(height, width)
+    h = _mix32(idx ^ np.uint64(seed & _M32)).astype(np.float64) / 4294967296.0
+    noise = 1.0 + 0.03 * (2.0 * h - 1.0)
+    img = np.empty((height, width, 4), np.float32)
+    img[..., 0] = lum * (0.6 + 0.4 * v) * noise
+    img[..., 1] = lum * (0.4 + 0.6 * (1 - v)) * noise
+    img[..., 2] = lum * (0.3 + 0.7 * np.abs(u - v)) * noise
+    hi = h > 0.995
+    img[hi, :3] *= 8.0
+    if signed:
+        sgn = np.where(_mix32(idx ^ np.uint64((seed * 7 + 3) & _M32)) & 1, -1.0, 1.0)
+        img[..., :3] *= sgn[..., None]
+    img[..., 3] = 1.0
+    return img

@@ -49,6 +49,8 @@ typedef enum TinyImageFormat {
     TinyImageFormat_DXBC2_SRGB,
     TinyImageFormat_DXBC3_UNORM,
     TinyImageFormat_DXBC3_SRGB,
+    TinyImageFormat_DXBC6H_UFLOAT,
+    TinyImageFormat_DXBC6H_SFLOAT,
     TinyImageFormat_Count
 } TinyImageFormat;
 

@@ -33,9 +33,13 @@ typedef enum gic_format {
     GIC_FMT_BC3 = 3, /* BC4-style alpha (:125) + 4-colour RGB half (amd_bc3_compressor.cpp:41-46) */
     GIC_FMT_BC4 = 4, /* Image_CompressAMDAlphaSingleModeBlock on one channel (:125) */
     GIC_FMT_BC5 = 5, /* two BC4 blocks, channel 0 then channel 1 (amd_bc5_compressor.cpp:35-41) */
+    GIC_FMT_BC6H = 6, /* BC6HBlockEncoder::CompressBlock, unsigned half floats (amd_bc6h_body.cpp:1521,
+                         Image_CompressAMDBC6H amd_bc6h_compressor.cpp:11 with an unsigned source) */
     GIC_FMT_BC7 = 7, /* BC7BlockEncoder::CompressBlock (amd_bc7_body.cpp:1289) */
-    GIC_FMT_BC7ENC16 = 8 /* BC7 blocks (modes 1/6) by bc7enc16, the reference's fast BC7 encoder
+    GIC_FMT_BC7ENC16 = 8, /* BC7 blocks (modes 1/6) by bc7enc16, the reference's fast BC7 encoder
                             (richgel999_bc7enc16.cpp:1517, Image_CompressRichGel999BC7 :21) */
+    GIC_FMT_BC6H_SF = 9 /* BC6H with the encoder's m_isSigned set (a signed source such as
+                           R32G32B32A32_SFLOAT, amd_bc6h_compressor.cpp:19-25) */
 } gic_format;
 
 /* Texel encodings of a source image (what Image_GetPixelAtF decodes). */
@@ -94,7 +98,7 @@ uint32_t gic_block_bytes(gic_format fmt);
  *          bytes (1..4, R[G[B[A]]]), slice pitch = row_pitch * height.
  *   d_dst: blocks in row-major order per slice, slices stacked
  *          (ceil(w/4) * ceil(h/4) * slices * gic_block_bytes).
- *   d_block_err: optional (NULL) per-block error (BC7: the encoder's error).
+ *   d_block_err: optional (NULL) per-block error (BC7 / BC6H: the encoder's error, 0 for the others).
  * Partial edge blocks replicate the last row/column (block_utils.cpp:19-22).
  * The launch is asynchronous on `stream`. */
 int gic_hip_encode(gic_format fmt, const uint8_t *d_src, uint32_t width, uint32_t height,
@@ -123,6 +127,8 @@ int gic_hip_encode_rows_src(gic_format fmt, gic_source src_type, const void *d_s
  *   BC1/BC2/BC3/BC7: d_blocks holds n x 64 floats (RGBA per texel, texel-major).
  *   BC4:     d_blocks holds n x 16 floats.
  *   BC7ENC16: n x 64 floats, each texel to RGBA8 as saturate(v) * 255 + 0.5.
+ *   BC6H / BC6H_SF: n x 64 floats (RGB used; any finite HDR value, converted to
+ *     half floats as CompressBlock does, amd_bc6h_body.cpp:1539-1573).
  * This is the batched form of the reference's block API
  * (imagecompress.h:111-136). */
 int gic_hip_encode_blocks_f32(gic_format fmt, const float *d_blocks, uint32_t n, const gic_options *opt,

@@ -91,6 +91,19 @@ int orc_encode_image_bc7_perf(const uint8_t *src, uint32_t width, uint32_t heigh
                               int32_t first_row, int32_t num_rows, int threads, float quality, uint8_t mode_mask,
                               float performance, uint8_t *dst, double *block_err);
 
+/* BC6HBlockEncoder::CompressBlock (amd_bc6h_body.cpp:1521-1652) as
+ * Image_CompressAMDBC6H constructs it (quality 1.0, amd_bc6h_compressor.cpp:28):
+ * in = 16 RGBA float texels (alpha ignored); returns the encoder's error.
+ * Parity-unpinned: Math_Float2Half is taken as IEEE binary16 RNE (orc_bc6h.c). */
+float orc_bc6h_block(const float in[64], int is_signed, uint8_t out[16]);
+int orc_encode_bc6h_blocks(const float *blocks, int n, int is_signed, int threads, uint8_t *out, float *err);
+/* test hooks: FindBestPattern of one pattern (-1 = one region), the half
+ * conversion, the BPTC anchors, eigenVector_d's squaring count */
+float orc_bc6h_pattern(const float in[64], int is_signed, int shape, float fep[12], int idx[32], int cnt[2]);
+uint16_t orc_float_to_half(float f);
+int orc_bc6h_anchor(int shape, int *pos);
+int orc_bc6h_ev_p(void);
+
 /* helpers exposed for unit tests */
 void orc_load_block_rgba8(const uint8_t *src, uint32_t width, uint32_t height,
                           uint32_t channels, uint32_t bx, uint32_t by,

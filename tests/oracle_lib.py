@@ -76,6 +76,17 @@ def lib() -> ctypes.CDLL:
                                                       ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int,
                                                       ctypes.c_int, ctypes.c_int, vp]
         _lib.orc_encode_image_bc7enc_rows.restype = ctypes.c_int
+        _lib.orc_encode_bc6h_blocks.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp]
+        _lib.orc_encode_bc6h_blocks.restype = ctypes.c_int
+        _lib.orc_bc6h_block.argtypes = [vp, ctypes.c_int, vp]
+        _lib.orc_bc6h_block.restype = ctypes.c_float
+        _lib.orc_float_to_half.argtypes = [ctypes.c_float]
+        _lib.orc_float_to_half.restype = ctypes.c_uint16
+        _lib.orc_bc6h_anchor.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+        _lib.orc_bc6h_anchor.restype = ctypes.c_int
+        _lib.orc_bc6h_ev_p.restype = ctypes.c_int
+        _lib.orc_bc6h_pattern.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp, vp]
+        _lib.orc_bc6h_pattern.restype = ctypes.c_float
     return _lib
 
 
@@ -221,6 +232,17 @@ def bc7enc_blocks(rgba: np.ndarray, fast: bool = False, perceptual: bool = True)
     for i in range(b.shape[0]):
         lib().orc_bc7enc_block(b[i].ctypes.data, int(fast), int(perceptual), out[i].ctypes.data)
     return out
+
+
+def bc6h_blocks(blocks: np.ndarray, signed: bool = False, threads: int = 0):
+    """BC6HBlockEncoder::CompressBlock (quality 1.0) on (n, 64) float RGBA blocks:
+    ((n, 16) uint8 blocks, (n,) float32 encoder errors)."""
+    b = np.ascontiguousarray(blocks, dtype=np.float32).reshape(-1, 64)
+    out = np.zeros((b.shape[0], 16), np.uint8)
+    err = np.zeros(b.shape[0], np.float32)
+    threads = threads or min(os.cpu_count() or 1, 16)
+    lib().orc_encode_bc6h_blocks(b.ctypes.data, b.shape[0], int(signed), threads, out.ctypes.data, err.ctypes.data)
+    return out, err
 
 
 def bc7_decode(blocks: np.ndarray) -> np.ndarray:

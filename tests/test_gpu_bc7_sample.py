@@ -191,3 +191,35 @@ def test_bc7_bounded_matches_model(gpu):
             done |= ok
         print(f"\n{w}x{h}: {100 * done.mean():.1f}% of blocks final after the probe")
         assert np.array_equal(got, model), _mismatch_report(got, model)
+
+
+def test_bc7_bounded_float_blocks_and_errors(gpu):
+    """The bounded path through the float block entry (gic_hip_encode_blocks_f32,
+    survivors compacted into lists of block ids like the image path) equals the
+    image path block for block and error for error; blocks outside the bound
+    carry the exact search's block and error (the oracle's)."""
+    import torch
+    g1 = synth.g1(8192, 8192)
+    img = np.ascontiguousarray(np.concatenate([g1[2048:2064, 512:768], _random_image()[120:136, :128]], axis=1))
+    h, w, _ = img.shape
+    nb = (w // 4) * (h // 4)
+    src = torch.from_numpy(img[None].copy()).cuda()
+    opts = gic.Options(bc7_mse_bound=MSE_ABS)
+    dst = torch.zeros(nb * 16, dtype=torch.uint8, device="cuda")
+    err = torch.zeros(nb, dtype=torch.float64, device="cuda")
+    gic.encode_device(7, src, w, h, 1, 4, dst, opts, block_err=err)
+    sb = _src_blocks(img)
+    fb = torch.from_numpy((sb.astype(np.float32) / np.float32(255.0)).reshape(nb, 64)).cuda()
+    dst2 = torch.zeros(nb * 16, dtype=torch.uint8, device="cuda")
+    err2 = torch.zeros(nb, dtype=torch.float64, device="cuda")
+    gic.encode_blocks_f32(gic.FMT_BC7, fb, dst2, opts, block_err=err2)
+    torch.cuda.synchronize()
+    got, got2 = dst.cpu().numpy().reshape(-1, 16), dst2.cpu().numpy().reshape(-1, 16)
+    e, e2 = err.cpu().numpy(), err2.cpu().numpy()
+    assert np.array_equal(got, got2), _mismatch_report(got, got2)
+    assert np.array_equal(e, e2)
+    ref, rerr = oracle_lib.encode_image_bc7(img, want_err=True)
+    full = _block_mse(got, sb) > MSE_ABS
+    assert full.any() and (~full).any()
+    assert np.array_equal(got[full], ref[full]), _mismatch_report(got[full], ref[full])
+    assert np.array_equal(e[full], rerr[full])

@@ -109,3 +109,39 @@ def test_bc7enc_oracle_decodes_close_to_source():
     solid[:, :, :3] = np.arange(256, dtype=np.uint8)[:, None, None]
     dec = oracle_lib.bc7_decode(oracle_lib.bc7enc_blocks(solid, fast=True, perceptual=False))
     assert np.abs(dec[:, :, :3].astype(int) - solid[:, :, :3]).max() <= 1
+
+
+def test_bc6h_oracle_helpers():
+    """The BC6H restatement's fixed pieces: IEEE half conversion (the assumed
+    Math_Float2Half) against numpy, the anchor tables derived from the BPTC
+    shapes against the reference's literal g_indexfixups / g_Region2FixUp
+    (amd_bc6h_body.hpp:194-220), eigenVector_d's squaring count."""
+    import ctypes
+    lib = oracle_lib.lib()
+    rng = np.random.default_rng(2)
+    xs = np.concatenate([rng.random(4000) * 70000, rng.random(2000) * 1e-4, np.exp2(rng.uniform(-30, 17, 2000)),
+                         [0.0, 6e-8, 5.96e-8, 65504.0, 65519.0, 65520.0, 1e30]]).astype(np.float32)
+    with np.errstate(over="ignore"):
+        want = xs.astype(np.float16).view(np.uint16)
+    got = np.array([lib.orc_float_to_half(float(x)) for x in xs], np.uint16)
+    assert np.array_equal(got, want)
+    fix = [15] * 16 + [15, 2, 8, 2, 2, 8, 8, 15, 2, 8, 2, 2, 8, 8, 2, 2]
+    r2 = [7, 3, 11, 7, 3, 11, 9, 5, 2, 12, 7, 3, 11, 7, 11, 3, 7, 1, 0, 1, 0, 1, 0, 7, 0, 1, 1, 0, 4, 4, 1, 0]
+    for s in range(32):
+        pos = ctypes.c_int()
+        assert lib.orc_bc6h_anchor(s, ctypes.byref(pos)) == fix[s]
+        assert pos.value == r2[s]
+    assert lib.orc_bc6h_ev_p() == 5
+
+
+def test_bc6h_oracle_blocks_are_valid():
+    """Oracle BC6H blocks carry a two-region mode (1..10: the one-region
+    pattern is never encoded, orc_bc6h.c) or the reference's red block."""
+    rng = np.random.default_rng(8)
+    blocks = (rng.random((64, 64)) * np.exp2(rng.uniform(-6, 3, size=(64, 1)))).astype(np.float32)
+    out, err = oracle_lib.bc6h_blocks(blocks)
+    two_bit = out[:, 0] & 3
+    five_bit = out[:, 0] & 0x1f
+    ok = (two_bit < 2) | np.isin(five_bit, [0x02, 0x06, 0x0a, 0x0e, 0x12, 0x16, 0x1a, 0x1e])
+    assert ok.all()
+    assert np.isfinite(err).all()
