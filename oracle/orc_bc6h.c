@@ -386,7 +386,7 @@ static const float kLerpW[5][16] = {   /* rampLerpWeights, amd_hdr_encode.cpp:16
      34.0f / 64.0f, 38.0f / 64.0f, 43.0f / 64.0f, 47.0f / 64.0f, 51.0f / 64.0f, 55.0f / 64.0f, 60.0f / 64.0f, 1.0f}};
 
 /* ep_df / expandbits_ with 8 bits (bits {8, 8, 8}): v | v >> 8 (:2098-2111) */
-static float ep8(int v) { return (float)((v << 0) | (v >> 8)); }
+static float ep8(int v) { return (float)(v | (v >> 8)); }   /* v << 0 == v (also for v < 0) */
 
 /* rampf (USE_NEWRAMP, :2113-2120) with 8-bit codes; clog = log2 of the ramp size */
 static float ramp8(int clog, int p1, int p2, int i)
