@@ -72,6 +72,8 @@ def parse():
                    help="BC7 bounded-exit legs: per-block MSE under which the probe's block is final (0 = no legs); "
                         "the batch64 workload uses this value too (0 = no exit)")
     p.add_argument("--no-bc7enc", action="store_true", help="skip the bc7enc16 (fast BC7 path) legs")
+    p.add_argument("--bc6h-size", type=int, default=1024,
+                   help="BC6H leg: HDR float32 texture width = height per rank (0 = skip the leg)")
     p.add_argument("--bc7-shake-ranks", type=int, default=None,
                    help="pruned BC7 search: partitions shaken per single-index mode (gic_options."
                         "bc7_shake_ranks).  8k workload: the pruned legs (default 2; 0 = skip them; the exact "
@@ -426,6 +428,54 @@ def bc7enc16_leg(args, gic, src, size, world, dev, rank, fast):
     return res
 
 
+def bc6h_leg(args, gic, world, dev, rank):
+    """BC6H (unsigned half floats, BC6HBlockEncoder at the
+    image API's quality 1.0) on a synthetic HDR float32 texture (synth.hdr_rgba:
+    12 stops, noise, highlights), steps x one launch over the rank's texture,
+    plus (rank 0) the CPU restatement on a bounded sample of blocks with a
+    bit-exactness check."""
+    import numpy as np
+    import torch
+    from gfx_imagecompress_amd import synth
+    n = args.bc6h_size
+    bx = by = (n + 3) // 4
+    img = synth.hdr_rgba(n, n, seed=1 + rank)
+    src = torch.from_numpy(img.reshape(-1).copy()).to(dev)
+    dst = torch.empty(bx * by * 16, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        gic.encode_device_src(gic.FMT_BC6H, gic.SRC_FLOAT32, src, n, n, 1, 4, dst, stream=stream)
+    step()
+    wall, kern_ms = _timed(world, dev, stream, step, max(1, min(args.steps, 3)))
+    steps = max(1, min(args.steps, 3))
+    res = {"metric": f"Mpixels/s BC6H (unsigned, quality 1.0) on a {n}x{n} synthetic HDR float32 texture",
+           "value": round(n * n * world * steps / wall / 1e6, 4), "unit": "Mpixels/s",
+           "blocks_per_s": round(bx * by * world * steps / wall, 1), "ms_per_step": round(wall / steps * 1e3, 3),
+           "kernel_ms": round(kern_ms, 3), "kernel_ms_rank_min_max": [round(x, 3) for x in _timed.spread],
+           "dtype": "f32", "steps": steps,
+           "roofline": {"bound": "valu", "alg_bytes_per_launch": 272 * bx * by,
+                        "hbm_frac": round(272 * bx * by / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 8),
+                        "note": "272 B per block: 256 B of float32 RGBA texels read, 16 B written"}}
+    if rank == 0 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        threads = _cpu_threads()
+        blocks = img[:16].reshape(4, 4, bx, 4, 4).transpose(0, 2, 1, 3, 4).reshape(-1, 64)   # block rows 0-3
+        nsamp = min(len(blocks), 1024)
+        c0 = time.perf_counter()
+        ref, _ = oracle_lib.bc6h_blocks(blocks[:nsamp], threads=threads)
+        dt = time.perf_counter() - c0
+        got = dst.cpu().numpy().reshape(-1, 16)[:nsamp]
+        res["cpu_baseline"] = {"value": round(nsamp * 16 / dt / 1e6, 5), "unit": "Mpixels/s", "cores": threads,
+                               "kind": "port", "cpu_model": cpu_model(),
+                               "sample": f"the first {nsamp} blocks of block row 0 ({dt:.2f} s, {threads} threads)",
+                               "blocks_per_s": round(nsamp / dt, 1)}
+        res["gpu_parity"] = "bit-exact" if np.array_equal(got, ref) else \
+            f"{int((got != ref).any(axis=1).sum())} blocks differ"
+    return res
+
+
 def _valu_roofline(name, size, rows, kern_ms):
     """VALU issue roofline of a kernel: SQ_INSTS_VALU per launch from the
     committed PMC summary profiles/<name> (tools/valu_json.py, same workload)
@@ -673,6 +723,8 @@ def main():
     if fmt == 1 and not args.no_bc45:
         for f in (4, 5):
             bc45[f"bc{f}"] = bc45_leg(args, gic, f, world, dev, rank)
+    if fmt == 1 and args.bc6h_size > 0:
+        bc45["bc6h"] = bc6h_leg(args, gic, world, dev, rank)
 
     cpu = None
     parity = None

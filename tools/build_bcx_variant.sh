@@ -9,5 +9,5 @@ cp $SRC csrc/_vb.hip
 /opt/rocm/bin/hipcc $F "$@" -c csrc/_vb.hip -o /tmp/_vb_$NAME.o
 rm -f csrc/_vb.hip
 mkdir -p ../gpurun_dbg/$NAME
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fPIC -o ../gpurun_dbg/$NAME/lib.so /tmp/_vb_$NAME.o build/gic_bc7.o build/gic_bc7enc.o build/gic_api.o
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fPIC -o ../gpurun_dbg/$NAME/lib.so /tmp/_vb_$NAME.o build/gic_bc7.o build/gic_bc7enc.o build/gic_bc6h.o build/gic_api.o
 echo built $NAME

@@ -11,6 +11,6 @@ cp ${QUANT_INC:-csrc/bc7_quant.inc} csrc/_v_quant.inc
 sed 's/#include "bc7_wave.inc"/#include "_v_wave.inc"/; s/#include "bc7_quant.inc"/#include "_v_quant.inc"/' $HIP > csrc/_v.hip
 /opt/rocm/bin/hipcc $F "$@" -c csrc/_v.hip -o /tmp/_v_bc7.o
 mkdir -p ../gpurun_dbg/$NAME
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fPIC -o ../gpurun_dbg/$NAME/lib.so build/gic_bcx.o /tmp/_v_bc7.o build/gic_bc7enc.o build/gic_api.o
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fPIC -o ../gpurun_dbg/$NAME/lib.so build/gic_bcx.o /tmp/_v_bc7.o build/gic_bc7enc.o build/gic_bc6h.o build/gic_api.o
 rm -f csrc/_v.hip csrc/_v_wave.inc csrc/_v_quant.inc
 echo built $NAME
