@@ -113,6 +113,7 @@ struct Workspace {
     uint4 *best_blk;       // [n] its packed block
     double *uerr;          // [n][kUMax] optQuantAnD_d error of each distinct subset problem (modes 0-3)
     uint64_t *uidx;        // [n][kUMax] its indices, 4 bits per texel of the subset (texel order)
+    uint8_t *prank;        // [n][6][8] partition of stable rank r of each single-index slot (k_rank)
 };
 
 __device__ __forceinline__ int expand_code(int bits, int v) { return (v << (8 - bits)) | (v >> (2 * bits - 8)); }
@@ -1548,6 +1549,33 @@ __global__ void __launch_bounds__(256, 2) k_quant_reg(Params p, Workspace ws, in
     ws.qidx[(size_t)b * kQuantTasks + task] = tidx;
 }
 
+// K1 of the bounded exit's mode-6 probe: one lane per block, the quantiser's
+// first projection and lattice rounding only (opt_quant_mask<4, true>): on G1
+// 98 % of the probe's blocks come out identical to starting from the full
+// optQuantAnD_d and the share within the bound is unchanged, for a
+// fraction of the cost; the probe's blocks are checked against the bound anyway.
+__global__ void __launch_bounds__(256) k_quant_probe6(Params p, Workspace ws)
+{
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= p.n) return;
+    const BlockMeta meta = ws.meta[b];
+    if (!mode_active(meta, p, 6) || (meta.flags & 3u) != 2u) return;
+    const float *tex = ws.tex + (size_t)b * 64;
+    uint32_t px[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const float4 v = *reinterpret_cast<const float4 *>(tex + i * 4);
+        px[i] = (uint32_t)v.x | ((uint32_t)v.y << 8) | ((uint32_t)v.z << 16) | ((uint32_t)v.w << 24);
+    }
+    int idx[16];
+    opt_quant_mask<4, true>(px, 0xFFFFu, 16, idx);
+    uint64_t tidx = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) tidx |= (uint64_t)(idx[i] & 15) << (4 * i);
+    ws.qerr[(size_t)b * kQuantTasks + 208] = 0.;
+    ws.qidx[(size_t)b * kQuantTasks + 208] = tidx;
+}
+
 // K1t (performance < 1): optQuantTrace_d for the partitions of the single-index
 // modes with at most 8 clusters (0-3, 7) of blocks whose range exceeds
 // 255 * performance (CompressSingleIndexBlock :606-633); overwrites what the
@@ -1761,6 +1789,32 @@ __device__ __forceinline__ int shake_sub(const ShakeResult *shk, int r, int s)
     return e < 0 ? ((int)(-1.0 - e) & 3) : s;
 }
 
+// K1c: stable partition ranks (sortProjection, amd_bc7_3dquant_vpc.cpp:138-150)
+// of each single-index slot, one wave per (block, slot), lane = partition;
+// the partitions of ranks 0..7 are stored for the shake waves (computed once
+// per slot instead of once per (rank, subset) wave)
+__global__ void __launch_bounds__(256) k_rank(Params p, Workspace ws)
+{
+    const uint32_t wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t b = wid / kShakeSlots;
+    const int slot = (int)(wid % kShakeSlots);
+    if (b >= p.n) return;
+    const int mode = kSlotMode[slot];
+    const BlockMeta meta = ws.meta[b];
+    if (!mode_active(meta, p, mode) || (meta.flags & 3u) != 2u) return;
+    const int nparts = mode_tries(p, mode);
+    const int att = mode_attempts(p, mode);
+    const int ln = wv::lane();
+    const double *qe = ws.qerr + (size_t)b * kQuantTasks + kSlotBase[slot];
+    const double v = ln < nparts ? qe[ln] : 0.0;
+    int rk = 0;
+    for (int o = 0; o < nparts; ++o) {
+        const double w = wv::bcast_d(v, o);
+        rk += (w - v < 0 || (!(w - v > 0) && !(w - v < 0) && o < ln)) ? 1 : 0;
+    }
+    if (ln < nparts && rk < att) ws.prank[((size_t)b * kShakeSlots + slot) * kShakeRanks + rk] = (uint8_t)ln;
+}
+
 // K2 (waves): one wavefront per (block, mode, rank, subset) shake problem of
 // an integral block
 template <int NC>
@@ -1778,19 +1832,11 @@ __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, c
     const ModeInfo &mi = kModes[mode];
     const int nparts = mode_tries(p, mode);   // partitions quantised and ranked
     if (rank >= mode_attempts(p, mode)) return;
-    // stable rank of every partition, lane = partition (sortProjection order)
+    // the partition of this rank (k_rank); lane L < rank holds the one of rank L
     const int ln = wv::lane();
-    int part, rk = 0;
-    {
-        const double *qe = ws.qerr + (size_t)b * kQuantTasks + kSlotBase[slot];
-        const double v = ln < nparts ? qe[ln] : 0.0;
-        for (int o = 0; o < nparts; ++o) {
-            const double w = wv::bcast_d(v, o);
-            rk += (w - v < 0 || (!(w - v > 0) && !(w - v < 0) && o < ln)) ? 1 : 0;
-        }
-        const unsigned long long hit = __ballot(ln < nparts && rk == rank);
-        part = hit ? __ffsll((long long)hit) - 1 : 0;
-    }
+    const uint8_t *pr = ws.prank + ((size_t)b * kShakeSlots + slot) * kShakeRanks;
+    const int part = nparts == 1 ? 0 : (int)pr[rank];   // mode 6: one partition (no k_rank in its probe stage)
+    const int lpart = ln < rank ? (int)pr[ln] : 0;
     const uint64_t qidx = ws.qidx[(size_t)b * kQuantTasks + kSlotBase[slot] + part];
     const ShakeCfg cfg = shake_cfg(mode, p.quality);
     const float *tex = ws.tex + (size_t)b * 64;
@@ -1805,8 +1851,8 @@ __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, c
     // reads the first occurrence.  (Two-subset shapes never repeat a mask.)
     if (mi.subsets == 3) {
         int key = 0x7fffffff;
-        if (ln < nparts && rk < rank) {
-            const uint32_t sh = dShape3[ln];
+        if (ln < rank) {
+            const uint32_t sh = dShape3[lpart];
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
                 const uint32_t x = sh ^ (0x55555555u * (uint32_t)j);
@@ -1815,7 +1861,7 @@ __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, c
                 z = (z | (z >> 2)) & 0x0f0f0f0fu;
                 z = (z | (z >> 4)) & 0x00ff00ffu;
                 z = (z | (z >> 8)) & 0x0000ffffu;
-                if (z == mask) key = wv::imin(key, rk * 4 + j);
+                if (z == mask) key = wv::imin(key, ln * 4 + j);
             }
         }
         key = wv::wmin(key);
@@ -2592,6 +2638,7 @@ static hipError_t get_state(uint32_t chunk, int nsets, DeviceState *&out)
         const size_t sz = align_up(n * 64 * sizeof(float)) + align_up(n * sizeof(BlockMeta)) +
                           align_up(n * kQuantTasks * sizeof(double)) + align_up(n * kQuantTasks * sizeof(uint64_t)) +
                           align_up(n * kShakeSlots * kShakeRanks * sizeof(ShakeResult)) +
+                          align_up(n * kShakeSlots * kShakeRanks) +
                           align_up(n * kDualTasks * sizeof(DualResult)) + align_up(n * kDualTasks * 2 * sizeof(uint64_t)) +
                           align_up(n * kDualTasks * 2 * sizeof(double)) + align_up(n * sizeof(double)) +
                           align_up(n * sizeof(uint4)) + align_up(n * kUMax * sizeof(double)) +
@@ -2610,6 +2657,8 @@ static hipError_t get_state(uint32_t chunk, int nsets, DeviceState *&out)
         p += align_up(n * kQuantTasks * sizeof(uint64_t));
         w.shk = (ShakeResult *)p;
         p += align_up(n * kShakeSlots * kShakeRanks * sizeof(ShakeResult));
+        w.prank = (uint8_t *)p;
+        p += align_up(n * kShakeSlots * kShakeRanks);
         w.dual = (DualResult *)p;
         p += align_up(n * kDualTasks * sizeof(DualResult));
         w.dqidx = (uint64_t *)p;
@@ -2649,7 +2698,9 @@ static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, h
             hipLaunchKernelGGL(k_quant_sub, dim3((uint32_t)((nu + wg - 1) / wg)), dim3(wg), 0, s, p, ws, g_nu);
             hipLaunchKernelGGL(k_quant_gather, dim3((uint32_t)((nq3 + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
         }
-        if ((sm & 0xC0u) == 0x40u) {   // mode 6 alone (the bounded-exit probe): one lane per block
+        if ((sm & 0xC0u) == 0x40u && p.probe) {   // the bounded exit's mode-6 probe: first projection only
+            hipLaunchKernelGGL(k_quant_probe6, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, p, ws);
+        } else if ((sm & 0xC0u) == 0x40u) {   // mode 6 alone: one lane per block
             hipLaunchKernelGGL(k_quant_reg<4>, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, p, ws, 208, 1);
         } else if (sm & 0xC0u) {
             hipLaunchKernelGGL(k_quant_reg<4>, dim3((uint32_t)((nq4 + wg - 1) / wg)), dim3(wg), 0, s, p, ws, 208, 65);
@@ -2660,6 +2711,10 @@ static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, h
         }
         const uint64_t ns = (uint64_t)p.n * kShakeSlots * kShakeRanks;
         if (!integral) hipLaunchKernelGGL(k_shake, dim3((uint32_t)((ns + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
+        if (sm & 0x8Fu) {   // partition ranks of the multi-partition modes (mode 6 has one partition)
+            const uint64_t nr = (uint64_t)p.n * kShakeSlots * 64;
+            hipLaunchKernelGGL(k_rank, dim3((uint32_t)((nr + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
+        }
         if ((sm & 0x03u) && wave_count<8>(p.att)) {
             const uint64_t nw8 = (uint64_t)p.n * wave_count<8>(p.att) * 64;
             hipLaunchKernelGGL(k_shake_wave<8>, dim3((uint32_t)((nw8 + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);

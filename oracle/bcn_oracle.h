@@ -104,6 +104,10 @@ uint16_t orc_float_to_half(float f);
 int orc_bc6h_anchor(int shape, int *pos);
 int orc_bc6h_ev_p(void);
 
+/* bounded-exit probe model: mode 6 starts its shake from the quantiser's
+ * first projection (thread-local switch; not the reference) */
+void orc_bc7_set_probe_init(int on);
+
 /* helpers exposed for unit tests */
 void orc_load_block_rgba8(const uint8_t *src, uint32_t width, uint32_t height,
                           uint32_t channels, uint32_t bx, uint32_t by,

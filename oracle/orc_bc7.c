@@ -404,6 +404,39 @@ static double opt_quant(double data[][4], int n, int ncl, int *index, double out
     return total_error(data, out, n, dim);
 }
 
+/* Probe study hook (not the reference): with t_probe_init set, mode 6 takes
+ * its initial indices from the first iteration of optQuantAnD_d alone (the
+ * principal-axis projection rounded by quant_AnD_Shell, no requantisation
+ * rounds) -- a candidate cheaper start for the bounded exit's mode-6 probe. */
+static __thread int t_probe_init;
+void orc_bc7_set_probe_init(int on) { t_probe_init = on; }
+
+static double opt_quant_first(double data[][4], int n, int ncl, int *index, int dim)
+{
+    double cen[64][4], mean[4], cov[4][4], prj[64], dir[4] = {0, 0, 0, 0};
+    for (int i = 0; i < dim; ++i) {
+        mean[i] = 0;
+        for (int k = 0; k < n; ++k) mean[i] += data[k][i];
+        mean[i] /= (double)n;
+        for (int k = 0; k < n; ++k) cen[k][i] = data[k][i] - mean[i];
+    }
+    for (int i = 0; i < dim; ++i)
+        for (int j = 0; j < dim; ++j) {
+            cov[i][j] = 0;
+            for (int k = 0; k < n; ++k) cov[i][j] += cen[k][i] * cen[k][j];
+        }
+    double t = 0;
+    for (int j = 0; j < dim; ++j) t += cov[j][j];
+    if (t < (1. / 256.)) {
+        for (int i = 0; i < n; ++i) index[i] = 0;
+        return 0.;
+    }
+    principal_vector(cov, dir, dim);
+    project(cen, n, dir, prj, dim);
+    lattice_round(prj, ncl, n, index);
+    return 0.;
+}
+
 /* test hook: optQuantAnD_d on caller data (n <= 64) */
 double orc_bc7_opt_quant(const double *data4, int n, int ncl, int *index, int dim)
 {
@@ -1317,7 +1350,9 @@ static double single_index(bc7_enc *e, double in[16][4], uint8_t out[16], int mo
             if (!cnt[s]) continue;
             int idx[16];
             double o[16][4];
-            if (e->clusters[0] > 8 || e->max_range <= e->quant_thr)
+            if (t_probe_init && mode == 6)
+                err += opt_quant_first(sub[s], cnt[s], e->clusters[0], idx, dim);
+            else if (e->clusters[0] > 8 || e->max_range <= e->quant_thr)
                 err += opt_quant(sub[s], cnt[s], e->clusters[0], idx, o, dim);
             else
                 err += opt_quant_trace(sub[s], cnt[s], e->clusters[0], idx, o, dim);

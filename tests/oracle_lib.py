@@ -76,6 +76,8 @@ def lib() -> ctypes.CDLL:
                                                       ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int,
                                                       ctypes.c_int, ctypes.c_int, vp]
         _lib.orc_encode_image_bc7enc_rows.restype = ctypes.c_int
+        _lib.orc_bc7_set_probe_init.argtypes = [ctypes.c_int]
+        _lib.orc_bc7_set_probe_init.restype = None
         _lib.orc_encode_bc6h_blocks.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp]
         _lib.orc_encode_bc6h_blocks.restype = ctypes.c_int
         _lib.orc_bc6h_block.argtypes = [vp, ctypes.c_int, vp]

@@ -166,8 +166,10 @@ def _mode_of(blocks):
 
 def test_bc7_bounded_matches_model(gpu):
     """The bounded path, block by block, is: the oracle's mode-6 search (no
-    colour restriction) with 2 partitions shaken if that decodes within the
-    bound, else its mode-3 search likewise, else mode 1, else the exact search."""
+    colour restriction; its shaker started from the quantiser's first
+    projection, the probe's shortcut) if that decodes within the bound, else
+    its mode-3 search with 2 partitions shaken likewise, else mode 1, else the
+    exact search."""
     import torch
     g1 = synth.g1(8192, 8192)   # the bench texture: most blocks end in the probe
     mixed = np.ascontiguousarray(np.concatenate([g1[2048:2064, 512:640], synth.g1(128, 16, seed=5)], axis=1))
@@ -185,7 +187,12 @@ def test_bc7_bounded_matches_model(gpu):
         model = oracle_lib.encode_image_bc7(img)
         done = np.zeros(nb, bool)
         for mode in (6, 3, 1):
-            cand = oracle_lib.bc7_blocks_ex(sb, mode_mask=1 << mode, colour_restrict=False, shake_ranks=2)
+            # the mode-6 probe starts its shaker from the quantiser's first projection (k_quant_probe6)
+            oracle_lib.lib().orc_bc7_set_probe_init(int(mode == 6))
+            try:
+                cand = oracle_lib.bc7_blocks_ex(sb, mode_mask=1 << mode, colour_restrict=False, shake_ranks=2)
+            finally:
+                oracle_lib.lib().orc_bc7_set_probe_init(0)
             ok = ~done & (_mode_of(cand) == mode) & (_block_mse(cand, sb) <= MSE_ABS)
             model[ok] = cand[ok]
             done |= ok
