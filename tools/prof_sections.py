@@ -24,7 +24,8 @@ torch.cuda.synchronize()
 lib.gic_debug_profile(buf, 0)
 names = {0: "c.collapse", 1: "c.ls", 2: "c.pass_setup", 3: "c.build_ramp", 4: "c.texels", 5: "c.tail",
          6: "c.combo/iter", 8: "w.collapse", 9: "w.ls", 10: "w.chan_setup", 11: "w.texels", 12: "w.reduce+comb",
-         13: "w.rq_tail", 14: "w.combo", 15: "w.rq_unpack+ramp", 16: "w.rq_nearest", 17: "w.rq_wsum"}
+         13: "w.rq_tail", 14: "w.combo", 15: "w.rq_unpack+ramp", 16: "w.rq_nearest", 17: "w.rq_wsum",
+         18: "c.moments", 19: "c.exp_table", 20: "w.moments", 21: "w.exp_table"}
 tot = sum(buf[i] for i in names)
 for i, nm in names.items():
     print(f"{nm:16s} {buf[i] / 1e9:10.3f} Gcyc {100.0 * buf[i] / tot:6.1f}%")
