@@ -1451,11 +1451,16 @@ __global__ void __launch_bounds__(256) k_quant(Params p, Workspace ws)
 // of modes 0-3's subset problems), so each distinct one is solved once and
 // k_quant_gather sums the per-partition errors in subset order, exactly as the
 // per-partition loop of CompressSingleIndexBlock (:582-641) does.
-__global__ void __launch_bounds__(256, 2) k_quant_sub(Params p, Workspace ws, int nu)
+// Grid: x = subset problem u (wave-uniform), y = 256-block group, lane = block.
+// Every lane of a wave solves the same subset shape, so its texels are loaded
+// compacted (slot k = the k-th member) and every member loop of the quantiser
+// runs exactly n iterations under uniform branches (SelPrefix) -- a lane per
+// (block, problem) paid all 16 texel slots of every loop with per-lane masks.
+// Consecutive workgroups share their 256 blocks' texels in cache.
+__global__ void __launch_bounds__(256, 2) k_quant_sub(Params p, Workspace ws)
 {
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t b = gid / (uint32_t)nu;
-    const int u = (int)(gid % (uint32_t)nu);
+    const int u = (int)blockIdx.x;
+    const uint32_t b = blockIdx.y * blockDim.x + threadIdx.x;
     if (b >= p.n) return;
     const BlockMeta meta = ws.meta[b];
     if ((meta.flags & 3u) != 2u) return;
@@ -1466,21 +1471,37 @@ __global__ void __launch_bounds__(256, 2) k_quant_sub(Params p, Workspace ws, in
         need = need || (mpart != 0xFFu && mode_active(meta, p, m) && (int)mpart < mode_tries(p, m));
     }
     if (!need) return;
-    const float *tex = ws.tex + (size_t)b * 64;
-    uint32_t px[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const float4 v = *reinterpret_cast<const float4 *>(tex + i * 4);
-        px[i] = (uint32_t)v.x | ((uint32_t)v.y << 8) | ((uint32_t)v.z << 16) | ((uint32_t)v.w << 24);
-    }
     const uint32_t pr = dUProb[u];
     const uint32_t mask = pr & 0xFFFFu;
-    int idx[16];
-    const double err = opt_quant_mask<3>(px, mask, 1 << (pr >> 16), idx);
-    uint64_t tidx = 0;
+    const int n = __popc(mask);
+    const float *tex = ws.tex + (size_t)b * 64;
+    uint32_t px[16];
+    {
+        uint32_t m = mask;
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-        if ((mask >> i) & 1u) tidx |= (uint64_t)(idx[i] & 15) << (4 * i);
+        for (int k = 0; k < 16; ++k) {
+            px[k] = 0;
+            if (k < n) {
+                const int t = __builtin_ctz(m);   // uniform
+                m &= m - 1;
+                const float4 v = *reinterpret_cast<const float4 *>(tex + t * 4);
+                px[k] = (uint32_t)v.x | ((uint32_t)v.y << 8) | ((uint32_t)v.z << 16) | ((uint32_t)v.w << 24);
+            }
+        }
+    }
+    int idx[16];
+    const double err = opt_quant_sel<3>(px, SelPrefix{n}, 1 << (pr >> 16), idx);
+    uint64_t tidx = 0;
+    {
+        uint32_t m = mask;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (k < n) {
+                const int t = __builtin_ctz(m);
+                m &= m - 1;
+                tidx |= (uint64_t)(idx[k] & 15) << (4 * t);
+            }
+    }
     ws.uerr[(size_t)b * kUMax + u] = err;
     ws.uidx[(size_t)b * kUMax + u] = tidx;
 }
@@ -2694,8 +2715,7 @@ static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, h
         if (!integral) hipLaunchKernelGGL(k_quant, dim3((uint32_t)((nq + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
         const uint64_t nq3 = (uint64_t)p.n * 208, nq4 = (uint64_t)p.n * 65;
         if (sm & 0x0Fu) {
-            const uint64_t nu = (uint64_t)p.n * g_nu;
-            hipLaunchKernelGGL(k_quant_sub, dim3((uint32_t)((nu + wg - 1) / wg)), dim3(wg), 0, s, p, ws, g_nu);
+            hipLaunchKernelGGL(k_quant_sub, dim3((uint32_t)g_nu, (p.n + wg - 1) / wg), dim3(wg), 0, s, p, ws);
             hipLaunchKernelGGL(k_quant_gather, dim3((uint32_t)((nq3 + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
         }
         if ((sm & 0xC0u) == 0x40u && p.probe) {   // the bounded exit's mode-6 probe: first projection only

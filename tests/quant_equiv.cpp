@@ -30,6 +30,21 @@ struct Trial {
 static uint32_t rng = 12345;
 static uint32_t nextr() { rng ^= rng << 13; rng ^= rng >> 17; rng ^= rng << 5; return rng; }
 
+// Every third trial runs the compacted form (SelPrefix, k_quant_sub): the
+// subset's texels moved to slots 0..n-1, indices scattered back.
+template <int DIM>
+GIC_HD double quant_prefix(const uint32_t px[16], uint32_t mask, int ncl, int idx[16])
+{
+    uint32_t pc[16];
+    int ic[16], n = 0;
+    for (int i = 0; i < 16; ++i) pc[i] = 0;
+    for (int i = 0; i < 16; ++i)
+        if ((mask >> i) & 1u) pc[n++] = px[i];
+    const double e = opt_quant_sel<DIM>(pc, SelPrefix{n}, ncl, ic);
+    for (int i = 0, k = 0; i < 16; ++i) idx[i] = ((mask >> i) & 1u) ? ic[k++] : 0;
+    return e;
+}
+
 #if defined(__HIPCC__)
 __global__ void k_equiv(const Trial *tr, int n, double *err, int *idx)
 {
@@ -39,7 +54,9 @@ __global__ void k_equiv(const Trial *tr, int n, double *err, int *idx)
     for (int i = 0; i < 16; ++i) px[i] = tr[t].px[i];
     int id[16];
     double e;
-    if (tr[t].mask == 0xffffu && tr[t].dim == 3)
+    if (t % 3 == 2)
+        e = tr[t].dim == 3 ? quant_prefix<3>(px, tr[t].mask, tr[t].ncl, id) : quant_prefix<4>(px, tr[t].mask, tr[t].ncl, id);
+    else if (tr[t].mask == 0xffffu && tr[t].dim == 3)
         e = opt_quant_mask<3>(px, 0xffffu, tr[t].ncl, id);   // constant mask, as k_dual_quant
     else if (tr[t].dim == 3)
         e = opt_quant_mask<3>(px, tr[t].mask, tr[t].ncl, id);
@@ -96,8 +113,12 @@ int main(int argc, char **argv)
     const long ff = -1;
 #else
     for (int t = 0; t < trials; ++t)
-        err[t] = tr[t].dim == 3 ? opt_quant_mask<3>(tr[t].px, tr[t].mask, tr[t].ncl, &idx[t * 16])
-                                : opt_quant_mask<4>(tr[t].px, tr[t].mask, tr[t].ncl, &idx[t * 16]);
+        if (t % 3 == 2)
+            err[t] = tr[t].dim == 3 ? quant_prefix<3>(tr[t].px, tr[t].mask, tr[t].ncl, &idx[t * 16])
+                                    : quant_prefix<4>(tr[t].px, tr[t].mask, tr[t].ncl, &idx[t * 16]);
+        else
+            err[t] = tr[t].dim == 3 ? opt_quant_mask<3>(tr[t].px, tr[t].mask, tr[t].ncl, &idx[t * 16])
+                                    : opt_quant_mask<4>(tr[t].px, tr[t].mask, tr[t].ncl, &idx[t * 16]);
     const long ff = g_ff;
 #endif
     int bad = 0;
