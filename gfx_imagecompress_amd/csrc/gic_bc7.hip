@@ -2109,13 +2109,15 @@ __global__ void __launch_bounds__(256, 4) k_dual_wave(Params p, Workspace ws, co
     const int bits[4] = {cb, cb, cb, half ? 6 * cb : 2 * 3 * cb};
     int epo[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
     const bool corners_too = !(meta.max_range > p.shake_thr);
+    wv::Round0 none;
+    none.valid = false;
     double e;
     if (last == 3) {
-        if (corners_too) wv::corners<4>(sp, T, idx, epo, last, bits, PAR_CART);   // Q9: error ignored
-        e = wv::window<4, 3>(sp, T, idx, epo, shake, last, bits[3]);
+        if (corners_too) wv::corners<4>(sp, T, idx, epo, last, bits, PAR_CART, none);   // Q9: error ignored
+        e = wv::window<4, 3>(sp, T, idx, epo, shake, last, bits[3], none);
     } else {
-        if (corners_too) wv::corners<8>(sp, T, idx, epo, last, bits, PAR_CART);
-        e = wv::window<8, 3>(sp, T, idx, epo, shake, last, bits[3]);
+        if (corners_too) wv::corners<8>(sp, T, idx, epo, last, bits, PAR_CART, none);
+        e = wv::window<8, 3>(sp, T, idx, epo, shake, last, bits[3], none);
     }
     unsigned long long ti = T.live ? (unsigned long long)(idx & 15) << (4 * ln) : 0ull;
 #pragma unroll

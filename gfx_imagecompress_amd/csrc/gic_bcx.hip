@@ -1173,7 +1173,7 @@ struct Bc1Params {
 };
 
 template <bool R3D>
-__global__ void __launch_bounds__(256, 2) bc1_image_kernel(Geometry g, Bc1Params p, uint2 *__restrict__ dst)
+__global__ void __launch_bounds__(256, 3) bc1_image_kernel(Geometry g, Bc1Params p, uint2 *__restrict__ dst)
 {
     __shared__ float lut[256];   // byte -> v / 255.0f
     lut[threadIdx.x] = (float)threadIdx.x / 255.0f;
