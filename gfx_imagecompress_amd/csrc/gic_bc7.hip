@@ -114,6 +114,8 @@ struct Workspace {
     double *uerr;          // [n][kUMax] optQuantAnD_d error of each distinct subset problem (modes 0-3)
     uint64_t *uidx;        // [n][kUMax] its indices, 4 bits per texel of the subset (texel order)
     uint8_t *prank;        // [n][6][8] partition of stable rank r of each single-index slot (k_rank)
+    uint64_t *pqidx;       // [n][6][8] its optQuantAnD_d indices (k_rank), so a shake wave's loads are independent
+    uint32_t *px;          // [n][16] texels packed R | G << 8 | B << 16 | A << 24 (integral blocks; k_prep)
 };
 
 __device__ __forceinline__ int expand_code(int bits, int v) { return (v << (8 - bits)) | (v >> (2 * bits - 8)); }
@@ -1335,7 +1337,7 @@ static uint32_t host_attempts(const Params &p, int cap)
     return att;
 }
 
-__device__ void prep_block(const float inN[64], const Params &p, float *tex, BlockMeta &meta)
+__device__ void prep_block(const float inN[64], const Params &p, float *tex, BlockMeta &meta, uint32_t *px)
 {
     int needs_alpha = 0, zero_one = 0;
     double bmin[4] = {1.7976931348623157e308, 1.7976931348623157e308, 1.7976931348623157e308,
@@ -1374,6 +1376,12 @@ __device__ void prep_block(const float inN[64], const Params &p, float *tex, Blo
     }
     meta.valid = valid;
     meta.max_range = mr;
+    // packed copy for the shake waves (meaningful for integral blocks only)
+    for (int i = 0; i < 16; ++i) {
+        uint32_t w = 0;
+        for (int j = 0; j < 4; ++j) w |= (uint32_t)fminf(fmaxf(tex[i * 4 + j], 0.f), 255.f) << (8 * j);
+        px[i] = w;
+    }
     // bit0: outside the implemented path (values outside [0,1] would need
     // optQuantTrace_d or index the reference's tables out of bounds);
     // bit1: texels are integers, so every shaker error is an exact int32
@@ -1388,7 +1396,7 @@ __global__ void __launch_bounds__(256) k_prep_image(Geometry g, Params p, Worksp
     block_coords(g, out_block(p, b), slice, by, bx);
     float blk[64];
     load_block(g, slice, by, bx, p.force_alpha_one != 0, blk);
-    prep_block(blk, p, ws.tex + (size_t)b * 64, ws.meta[b]);
+    prep_block(blk, p, ws.tex + (size_t)b * 64, ws.meta[b], ws.px + (size_t)b * 16);
 }
 
 __global__ void __launch_bounds__(256) k_prep_f32(const float *__restrict__ blocks, Params p, Workspace ws)
@@ -1398,7 +1406,7 @@ __global__ void __launch_bounds__(256) k_prep_f32(const float *__restrict__ bloc
     float blk[64];
     const size_t o = (size_t)out_block(p, b) * 64;
     for (int i = 0; i < 64; ++i) blk[i] = blocks[o + i];
-    prep_block(blk, p, ws.tex + (size_t)b * 64, ws.meta[b]);
+    prep_block(blk, p, ws.tex + (size_t)b * 64, ws.meta[b], ws.px + (size_t)b * 16);
 }
 
 __device__ __forceinline__ void task_mode(int task, int &mode, int &part)
@@ -1816,7 +1824,8 @@ __device__ __forceinline__ int shake_sub(const ShakeResult *shk, int r, int s)
 // per slot instead of once per (rank, subset) wave)
 __global__ void __launch_bounds__(256) k_rank(Params p, Workspace ws)
 {
-    const uint32_t wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    // wave-uniform by construction; readfirstlane lets the compiler see it (scalar loads and branches)
+    const uint32_t wid = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t b = wid / kShakeSlots;
     const int slot = (int)(wid % kShakeSlots);
     if (b >= p.n) return;
@@ -1833,7 +1842,11 @@ __global__ void __launch_bounds__(256) k_rank(Params p, Workspace ws)
         const double w = wv::bcast_d(v, o);
         rk += (w - v < 0 || (!(w - v > 0) && !(w - v < 0) && o < ln)) ? 1 : 0;
     }
-    if (ln < nparts && rk < att) ws.prank[((size_t)b * kShakeSlots + slot) * kShakeRanks + rk] = (uint8_t)ln;
+    if (ln < nparts && rk < att) {
+        const size_t r = ((size_t)b * kShakeSlots + slot) * kShakeRanks + rk;
+        ws.prank[r] = (uint8_t)ln;
+        ws.pqidx[r] = ws.qidx[(size_t)b * kQuantTasks + kSlotBase[slot] + ln];
+    }
 }
 
 // K2 (waves): one wavefront per (block, mode, rank, subset) shake problem of
@@ -1841,30 +1854,37 @@ __global__ void __launch_bounds__(256) k_rank(Params p, Workspace ws)
 template <int NC>
 __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, const SpEntry *__restrict__ sp)
 {
-    const uint32_t wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    // wave-uniform by construction; readfirstlane lets the compiler see it (scalar loads and branches)
+    const uint32_t wid = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t per = (uint32_t)wave_count<NC>(p.att);
     const uint32_t b = wid / per;
     if (b >= p.n) return;
     int slot, rank, subset;
     wave_problem<NC>(p, (int)(wid % per), slot, rank, subset);
     const int mode = kSlotMode[slot];
+    const int nparts = mode_tries(p, mode);   // partitions quantised and ranked
+    const int ln = wv::lane();
+    // Every load the wave needs is issued here, before any of them is waited
+    // for: the block's meta, the partition of this rank and of the lower ranks
+    // (k_rank), its quantiser indices (k_rank's copy) and the packed texels
+    // (lane t < 16: texel t).  (Chained -- meta, then the partition, then its
+    // indices, then the subset's texels -- the loads left the shake waves
+    // waiting on memory for several microseconds each.)
+    const size_t sr = ((size_t)b * kShakeSlots + slot) * kShakeRanks;
     const BlockMeta meta = ws.meta[b];
+    // mode 6: one partition (no k_rank in its probe stage)
+    const int part = nparts == 1 ? 0 : (int)ws.prank[sr + rank];
+    const uint64_t qidx = nparts == 1 ? ws.qidx[(size_t)b * kQuantTasks + kSlotBase[slot]] : ws.pqidx[sr + rank];
+    const int lpart = ln < rank ? (int)ws.prank[sr + ln] : 0;   // lane L < rank: the partition of rank L
+    const uint32_t pxl = ln < 16 ? ws.px[(size_t)b * 16 + ln] : 0u;
     if (!mode_active(meta, p, mode) || (meta.flags & 3u) != 2u) return;
     const ModeInfo &mi = kModes[mode];
-    const int nparts = mode_tries(p, mode);   // partitions quantised and ranked
     if (rank >= mode_attempts(p, mode)) return;
-    // the partition of this rank (k_rank); lane L < rank holds the one of rank L
-    const int ln = wv::lane();
-    const uint8_t *pr = ws.prank + ((size_t)b * kShakeSlots + slot) * kShakeRanks;
-    const int part = nparts == 1 ? 0 : (int)pr[rank];   // mode 6: one partition (no k_rank in its probe stage)
-    const int lpart = ln < rank ? (int)pr[ln] : 0;
-    const uint64_t qidx = ws.qidx[(size_t)b * kQuantTasks + kSlotBase[slot] + part];
     const ShakeCfg cfg = shake_cfg(mode, p.quality);
-    const float *tex = ws.tex + (size_t)b * 64;
     // gather the subset: lane L < n holds the L-th texel of the subset
     uint32_t mask = 0;
     for (int t = 0; t < 16; ++t) mask |= ((int)shape_of(mi.subsets, part, t) == subset ? 1u : 0u) << t;
-    ShakeResult &res = ws.shk[((size_t)b * kShakeSlots + slot) * kShakeRanks + rank];
+    ShakeResult &res = ws.shk[sr + rank];
     // Repeated problem (exact): three-subset shapes share subset masks, and a
     // subset's quantiser indices and shake depend only on its texels, so when a
     // lower rank of this mode shakes a subset with the same mask the result is
@@ -1904,9 +1924,8 @@ __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, c
                 cnt++;
             }
     }
-    unsigned px = 0;
-    if (ln < n)
-        for (int j = 0; j < cfg.dim; ++j) px |= (unsigned)tex[src * 4 + j] << (8 * j);
+    // lane L < n takes texel src (channels past dim are cleared by make_texels)
+    const unsigned px = (unsigned)__builtin_amdgcn_ds_bpermute(src * 4, (int)pxl);
     wv::Texels T;
     wv::make_texels(T, px, n, cfg.dim);
     int idx = T.live ? (int)((qidx >> (4 * src)) & 15u) : 0;
@@ -2079,7 +2098,8 @@ __global__ void __launch_bounds__(64) k_dual_quant_trace(Params p, Workspace ws)
 // (CompressDualIndexBlock :1158-1254); integral blocks
 __global__ void __launch_bounds__(256, 4) k_dual_wave(Params p, Workspace ws, const SpEntry *__restrict__ sp)
 {
-    const uint32_t wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    // wave-uniform by construction; readfirstlane lets the compiler see it (scalar loads and branches)
+    const uint32_t wid = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t b = wid / (kDualTasks * 2), r = wid % (kDualTasks * 2);
     if (b >= p.n) return;
     const uint32_t task = r >> 1, half = r & 1;
@@ -2665,7 +2685,8 @@ static hipError_t get_state(uint32_t chunk, int nsets, DeviceState *&out)
                           align_up(n * kDualTasks * sizeof(DualResult)) + align_up(n * kDualTasks * 2 * sizeof(uint64_t)) +
                           align_up(n * kDualTasks * 2 * sizeof(double)) + align_up(n * sizeof(double)) +
                           align_up(n * sizeof(uint4)) + align_up(n * kUMax * sizeof(double)) +
-                          align_up(n * kUMax * sizeof(uint64_t));
+                          align_up(n * kUMax * sizeof(uint64_t)) +
+                          align_up(n * kShakeSlots * kShakeRanks * sizeof(uint64_t)) + align_up(n * 16 * sizeof(uint32_t));
         e = hipMalloc(&st.ws_mem[k], sz);
         if (e != hipSuccess) return e;
         Workspace &w = st.ws[k];
@@ -2695,6 +2716,10 @@ static hipError_t get_state(uint32_t chunk, int nsets, DeviceState *&out)
         w.uerr = (double *)p;
         p += align_up(n * kUMax * sizeof(double));
         w.uidx = (uint64_t *)p;
+        p += align_up(n * kUMax * sizeof(uint64_t));
+        w.pqidx = (uint64_t *)p;
+        p += align_up(n * kShakeSlots * kShakeRanks * sizeof(uint64_t));
+        w.px = (uint32_t *)p;
         st.ws_blocks[k] = chunk;
     }
     out = &st;
