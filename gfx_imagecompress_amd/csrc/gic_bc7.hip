@@ -2106,22 +2106,23 @@ __global__ void __launch_bounds__(256, 4) k_dual_wave(Params p, Workspace ws, co
     const int mode = task < 8 ? 4 : 5;
     const int rot = task < 8 ? (int)(task >> 1) : (int)(task - 8);
     const int sel = task < 8 ? (int)(task & 1) : 0;
-    const BlockMeta meta = ws.meta[b];
-    if (!mode_active(meta, p, mode) || (meta.flags & 3u) != 2u) return;
     const int ln = wv::lane();
+    // loads issued before any is waited for (as in k_shake_wave)
+    const BlockMeta meta = ws.meta[b];
+    const uint32_t pxl = ln < 16 ? ws.px[(size_t)b * 16 + ln] : 0u;   // lane t < 16: texel t, packed
+    const uint64_t qi = ws.dqidx[((size_t)b * kDualTasks + task) * 2 + half];
+    if (!mode_active(meta, p, mode) || (meta.flags & 3u) != 2u) return;
     if (!dual_shaken(p, ws, b, (int)task)) {   // not shaken: never selected
         if (ln == 0) ws.dual[(size_t)b * kDualTasks + task].err[half] = 1.7976931348623157e308;
         return;
     }
     const int shake = dual_shake_size(p);
     const ModeInfo &mi = kModes[mode];
-    const float *tex = ws.tex + (size_t)b * 64;
     unsigned px = 0;
-    if (ln < 16)
-        for (int j = 0; j < 3; ++j) px |= (unsigned)tex[ln * 4 + kRot[rot][half ? 0 : j + 1]] << (8 * j);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) px |= ((pxl >> (8 * kRot[rot][half ? 0 : j + 1])) & 255u) << (8 * j);
     wv::Texels T;
     wv::make_texels(T, px, 16, 3);
-    const uint64_t qi = ws.dqidx[((size_t)b * kDualTasks + task) * 2 + half];
     int idx = T.live ? (int)((qi >> (4 * ln)) & 15u) : 0;
     const int ib = dual_index_bits(mi, (int)half, sel);
     const int last = (1 << ib) - 1;
