@@ -479,133 +479,151 @@ __device__ __forceinline__ float ramp8(float a, float b, int i)
 }
 
 // ep_shaker_HD (amd_hdr_encode.cpp:2280-2614) for one subset, dimension 3,
-// bits {8, 8, 8}, Mi_ = n - 1, CLOG = floor(log2(n)); exactly one round.
-// idx (texel-indexed) is updated in place like the reference's index_.
+// bits {8, 8, 8}, Mi_ = n - 1, CLOG = floor(log2(n)); exactly one round --
+// one wavefront per (block, shape, subset).  Lanes t < 16 hold texel t (x[3],
+// its quantiser index); the subset's members are visited in texel order with
+// readlane broadcasts wherever the reference sums in member order (cluster
+// means, the least-squares moments, each corner's error), so every float sum
+// is the reference's sequence.  The 64-corner walk runs one corner per lane:
+// corner p1's state s is gray(p1), and the walk's first strictly smaller error
+// is the minimum of (error bits, p1) -- the errors are sums of squares, so
+// their bit patterns order like their values.  (One lane per (block,
+// pattern) walking the corners serially held 3 x 8 ramps x 16 texels of
+// temporaries: 512 registers, one wave per SIMD, spills.)
+__device__ __forceinline__ float rbf(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+__device__ __forceinline__ int rbi(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+struct ShakeOut {        // ep_shaker_HD's result for one (block, shape, subset)
+    float err;
+    int epo[2][3];      // end point codes
+    uint32_t pad;
+    uint64_t idx;       // member texels' indices, 4 bits per texel (0 elsewhere)
+};
+
+// wave minimum of a non-negative float error and the lowest lane holding it
+__device__ __forceinline__ float wave_first_min(float e, int &lane_of)
+{
+    uint32_t u = __float_as_uint(e);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t v = (uint32_t)__shfl_xor((int)u, o);
+        u = v < u ? v : u;
+    }
+    lane_of = __builtin_ctzll(__ballot(__float_as_uint(e) == u));
+    return __uint_as_float(u);
+}
+
 template <int CLOG>
-__device__ __forceinline__ float shaker_hd(const float din[16][3], uint32_t mask, int n, int idx[16], int epo[2][3])
+__device__ void shake_hd_wave(const float x[3], int idxt, uint32_t mask, ShakeOut &out)
 {
     constexpr int NCL = 1 << CLOG;
+    const int L = (int)__lane_id();
+    const bool mem = L < 16 && ((mask >> L) & 1u);
+    const int n = __popc(mask);
     const int Mi_ = n - 1;
-    bool alls = true;
-    int f0 = -1;
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-        if ((mask >> i) & 1u) {
-            if (f0 < 0) f0 = i;
-        }
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-        if ((mask >> i) & 1u)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                float d0 = din[0][j];
-#pragma unroll
-                for (int u = 1; u < 16; ++u) d0 = u == f0 ? din[u][j] : d0;
-                alls = alls && d0 == din[i][j];
-            }
+    const int f0 = __builtin_ctz(mask);
+    // all members equal to the first (exact compares)
+    const float y0 = rbf(x[0], f0), y1 = rbf(x[1], f0), y2 = rbf(x[2], f0);
+    const bool alls = __all(!mem || (x[0] == y0 && x[1] == y1 && x[2] == y2));
     // index_collapse_kernel (:1688-1713)
-    int cidx0[16];
     int mi = 0x7fffffff, Mx = -0x7fffffff;
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-        if ((mask >> k) & 1u) {
-            mi = mi < idx[k] ? mi : idx[k];
-            Mx = Mx > idx[k] ? Mx : idx[k];
-        }
+    for (uint32_t mm = mask; mm; mm &= mm - 1) {
+        const int v = rbi(idxt, __builtin_ctz(mm));
+        mi = mi < v ? mi : v;
+        Mx = Mx > v ? Mx : v;
+    }
     int D = 1;
-    for (int d = 2; d <= Mx - mi; d++) {
-        bool all = true;
-#pragma unroll
-        for (int k = 0; k < 16; k++)
-            if ((mask >> k) & 1u) all = all && ((idx[k] - mi) % d == 0);
-        if (all) D = d;
-    }
-    int Mi = 0;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        cidx0[k] = ((mask >> k) & 1u) ? (idx[k] - mi) / D : 0;
-        Mi = Mi > cidx0[k] ? Mi : cidx0[k];
-    }
+    for (int d = 2; d <= Mx - mi; d++)
+        if (__all(!mem || (idxt - mi) % d == 0)) D = d;
+    const int c0 = mem ? (idxt - mi) / D : 0;
+    const int Mi = (Mx - mi) / D;
     float err_o = 3.402823466e+38f;
+    int idx_new = idxt;
+    uint64_t idx_o = 0;
+    bool took = false;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) out.epo[i][j] = 0;
     if (Mi == 0) {
         // quant_single_point_d without USE_RAMPS: index 0, end points 0, out 0
         float t = 0;
         if (!alls)
+            for (uint32_t mm = mask; mm; mm &= mm - 1) {
+                const int u = __builtin_ctz(mm);
 #pragma unroll
-            for (int i = 0; i < 16; ++i)
-                if ((mask >> i) & 1u)
-#pragma unroll
-                    for (int j = 0; j < 3; ++j) t += (din[i][j] - 0.0f) * (din[i][j] - 0.0f);
+                for (int j = 0; j < 3; ++j) {
+                    const float v = rbf(x[j], u);
+                    t += (v - 0.0f) * (v - 0.0f);
+                }
+            }
         if (t < err_o) {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) idx[k] = 0;
-#pragma unroll
-            for (int j = 0; j < 3; ++j) epo[0][j] = epo[1][j] = 0;
+            idx_new = 0;
             err_o = t;
         }
-        return err_o;
-    }
-    float err_2 = 3.402823466e+38f;
-    uint64_t idx_2 = 0;
-    int epo_2[2][3] = {{0, 0, 0}, {0, 0, 0}};
-    for (int q = 1; q * Mi <= Mi_; q++)
-        for (int p = 0; p <= Mi_ - q * Mi; p++) {
-            // least squares on the rounded cluster means (:2377-2437)
-            float im00 = 0, im01 = 0, im11 = 0, rp[2][3] = {{0, 0, 0}, {0, 0, 0}};
+    } else {
+        // cluster_mean_d_d for this lane's cluster: members in texel order
+        float cc[3] = {0.f, 0.f, 0.f};
+        {
+            float sm[3] = {0.f, 0.f, 0.f};
+            int cnt = 0;
+            for (uint32_t mm = mask; mm; mm &= mm - 1) {
+                const int u = __builtin_ctz(mm);
+                const bool same = rbi(c0, u) == c0;
+                cnt += same ? 1 : 0;
 #pragma unroll
-            for (int k = 0; k < 16; ++k)
-                if ((mask >> k) & 1u) {
-                    const int ck = cidx0[k] * q + p;
-                    // cluster_mean_d_d: the members of this cluster in texel order
-                    float sm[3] = {0, 0, 0};
-                    int cnt = 0;
+                for (int j = 0; j < 3; ++j) {
+                    const float v = rbf(x[j], u);
+                    sm[j] = same ? sm[j] + v : sm[j];
+                }
+            }
+            if (mem)
 #pragma unroll
-                    for (int u = 0; u < 16; ++u)
-                        if (((mask >> u) & 1u) && cidx0[u] == cidx0[k]) {
-                            ++cnt;
-#pragma unroll
-                            for (int j = 0; j < 3; ++j) sm[j] += din[u][j];
-                        }
+                for (int j = 0; j < 3; ++j) cc[j] = floorf(sm[j] / (float)cnt + 0.5f);
+        }
+        const int s = L ^ (L >> 1);   // the walk's state after step p1 = L
+        float err_2 = 3.402823466e+38f;
+        uint64_t idx_2 = 0;
+        int epo_2[2][3] = {{0, 0, 0}, {0, 0, 0}};
+        for (int q = 1; q * Mi <= Mi_; q++)
+            for (int p = 0; p <= Mi_ - q * Mi; p++) {
+                // least squares on the rounded cluster means (:2377-2437), member order
+                float im00 = 0, im01 = 0, im11 = 0, rp[2][3] = {{0, 0, 0}, {0, 0, 0}};
+                for (uint32_t mm = mask; mm; mm &= mm - 1) {
+                    const int u = __builtin_ctz(mm);
+                    const int ck = rbi(c0, u) * q + p;
                     im00 += (float)((Mi_ - ck) * (Mi_ - ck));
                     im01 += (float)(ck * (Mi_ - ck));
                     im11 += (float)(ck * ck);
 #pragma unroll
                     for (int j = 0; j < 3; ++j) {
-                        const float cc = floorf(sm[j] / (float)cnt + 0.5f);
-                        rp[0][j] += (float)(Mi_ - ck) * cc;
-                        rp[1][j] += (float)ck * cc;
+                        const float c = rbf(cc[j], u);
+                        rp[0][j] += (float)(Mi_ - ck) * c;
+                        rp[1][j] += (float)ck * c;
                     }
                 }
-            const float dd = im00 * im11 - im01 * im01;
-            const float i10 = im00;
-            const float a00 = im11 / dd, a11 = i10 / dd, a01 = -im01 / dd;
-            float epd[2][3][2];
+                const float dd = im00 * im11 - im01 * im01;
+                const float i10 = im00;
+                const float a00 = im11 / dd, a11 = i10 / dd, a01 = -im01 / dd;
+                float epd[2][3][2], eq[2][3][2];
 #pragma unroll
-            for (int j = 0; j < 3; j++) {
-                const float e0 = (a00 * rp[0][j] + a01 * rp[1][j]) * (float)Mi_;
-                const float e1 = (a01 * rp[0][j] + a11 * rp[1][j]) * (float)Mi_;
-                epd[0][j][0] = epd[0][j][1] = e0;
-                epd[1][j][0] = epd[1][j][1] = e1;
+                for (int j = 0; j < 3; j++) {
+                    const float e0 = (a00 * rp[0][j] + a01 * rp[1][j]) * (float)Mi_;
+                    const float e1 = (a01 * rp[0][j] + a11 * rp[1][j]) * (float)Mi_;
+                    epd[0][j][0] = epd[0][j][1] = e0;
+                    epd[1][j][0] = epd[1][j][1] = e1;
 #pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    const int lim = (int)(255u - (uint32_t)cvt_i32(epd[i][j][1]));
-                    epd[i][j][1] += (float)(lim < 1 ? lim : 1);
+                    for (int i = 0; i < 2; ++i) {
+                        const int lim = (int)(255u - (uint32_t)cvt_i32(epd[i][j][1]));
+                        epd[i][j][1] += (float)(lim < 1 ? lim : 1);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int c = 0; c < 2; ++c) eq[i][j][c] = ep8(cvt_i32(epd[i][j][c]));
                 }
-            }
-            // the 64-corner walk (:2476-2549): corner s takes, per channel j,
-            // end point 0's candidate (s >> 2j) & 1 and end point 1's (s >> 2j+1) & 1
-            float eq[2][3][2];   // their expanded codes
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 3; ++j)
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) eq[i][j][c] = ep8(cvt_i32(epd[i][j][c]));
-            float err_1 = 3.402823466e+38f;
-            uint64_t idx_1 = 0;
-            int s1 = 0, s = 0;
-            for (int p1 = 0; p1 < 64; p1++) {
-                s ^= p1 & (-p1);
+                // corner s of the 64-corner walk (:2476-2549): per channel j, end
+                // point 0's candidate (s >> 2j) & 1 and end point 1's (s >> 2j+1) & 1
                 float R[3][NCL];
 #pragma unroll
                 for (int j = 0; j < 3; ++j) {
@@ -616,63 +634,62 @@ __device__ __forceinline__ float shaker_hd(const float din[16][3], uint32_t mask
                 }
                 float err_0 = 0;
                 uint64_t idx_0 = 0;
+                for (uint32_t mm = mask; mm; mm &= mm - 1) {
+                    const int i = __builtin_ctz(mm);
+                    const float d0 = rbf(x[0], i), d1 = rbf(x[1], i), d2 = rbf(x[2], i);
+                    int ci = 0;
+                    float cmin = 3.402823466e+38f;
 #pragma unroll
-                for (int i = 0; i < 16; i++)
-                    if ((mask >> i) & 1u) {
-                        int ci = 0;
-                        float cmin = 3.402823466e+38f;
-#pragma unroll
-                        for (int c = 0; c < NCL; c++) {
-                            const float r0 = R[0][c] - din[i][0], r1 = R[1][c] - din[i][1], r2 = R[2][c] - din[i][2];
-                            float t_ = 0.f;
-                            t_ += r0 * r0;
-                            t_ += r1 * r1;
-                            t_ += r2 * r2;
-                            if (t_ < cmin) {
-                                cmin = t_;
-                                ci = c;
-                            }
+                    for (int c = 0; c < NCL; c++) {
+                        const float r0 = R[0][c] - d0, r1 = R[1][c] - d1, r2 = R[2][c] - d2;
+                        float t_ = 0.f;
+                        t_ += r0 * r0;
+                        t_ += r1 * r1;
+                        t_ += r2 * r2;
+                        if (t_ < cmin) {
+                            cmin = t_;
+                            ci = c;
                         }
-                        idx_0 |= (uint64_t)ci << (4 * i);
-                        err_0 += cmin;
                     }
-                if (err_0 < err_1) {
-                    idx_1 = idx_0;
-                    err_1 = err_0;
-                    s1 = s;
+                    idx_0 |= (uint64_t)ci << (4 * i);
+                    err_0 += cmin;
+                }
+                int w;
+                const float err_1 = wave_first_min(err_0, w);
+                if (err_1 < err_2) {
+                    err_2 = err_1;
+                    const uint32_t lo = (uint32_t)rbi((int)(uint32_t)idx_0, w), hi = (uint32_t)rbi((int)(uint32_t)(idx_0 >> 32), w);
+                    idx_2 = ((uint64_t)hi << 32) | lo;
+                    const int s1 = w ^ (w >> 1);
+#pragma unroll
+                    for (int j = 0; j < 3; j++) {
+                        epo_2[0][j] = cvt_i32(epd[0][j][(s1 >> (2 * j)) & 1]);
+                        epo_2[1][j] = cvt_i32(epd[1][j][(s1 >> (2 * j + 1)) & 1]);
+                    }
                 }
             }
-            if (err_1 < err_2) {
-                idx_2 = idx_1;
-                err_2 = err_1;
+        if (err_2 < err_o) {
+            took = true;
+            idx_o = idx_2;
 #pragma unroll
-                for (int j = 0; j < 3; j++) {
-                    epo_2[0][j] = cvt_i32(epd[0][j][(s1 >> (2 * j)) & 1]);
-                    epo_2[1][j] = cvt_i32(epd[1][j][(s1 >> (2 * j + 1)) & 1]);
-                }
+            for (int j = 0; j < 3; j++) {
+                out.epo[0][j] = epo_2[0][j];
+                out.epo[1][j] = epo_2[1][j];
             }
+            err_o = err_2;
         }
-    if (err_2 < err_o) {
-#pragma unroll
-        for (int k = 0; k < 16; ++k)
-            if ((mask >> k) & 1u) idx[k] = nib(idx_2, k);
-#pragma unroll
-        for (int j = 0; j < 3; j++) {
-            epo[0][j] = epo_2[0][j];
-            epo[1][j] = epo_2[1][j];
-        }
-        err_o = err_2;
     }
-    return err_o;
-}
-
-__device__ __forceinline__ float shaker_dispatch(const float din[16][3], uint32_t mask, int idx[16], int epo[2][3])
-{
-    const int n = __popc(mask);
-    if (n >= 8) return shaker_hd<3>(din, mask, n, idx, epo);
-    if (n >= 4) return shaker_hd<2>(din, mask, n, idx, epo);
-    if (n >= 2) return shaker_hd<1>(din, mask, n, idx, epo);
-    return shaker_hd<0>(din, mask, n, idx, epo);
+    if (!took) {   // the members' indices as they stand (quantiser's, or 0 from the single point)
+        uint64_t v = 0;
+        for (uint32_t mm = mask; mm; mm &= mm - 1) {
+            const int u = __builtin_ctz(mm);
+            v |= (uint64_t)(rbi(idx_new, u) & 15) << (4 * u);
+        }
+        idx_o = v;
+    }
+    out.err = err_o;
+    out.idx = idx_o;
+    out.pad = 0;
 }
 
 // ---------------------------------------------------------- block loading ---
@@ -798,51 +815,149 @@ __device__ __forceinline__ float shape_error(const float din[16][3], uint32_t m1
     return total;
 }
 
-// K1: FindBestPattern for (block, pattern)
-__global__ void __launch_bounds__(256) k_bc6h_pattern(Src src, uint32_t first, uint32_t n, int is_signed,
-                                                      PatternState *__restrict__ ws)
+// FindBestPattern (:904-1037) in four launches per chunk:
+//   K0 k_bc6h_prep    lane / block: CompressBlock's texel conversion (f2h) into
+//                     the din workspace (every later kernel reads it);
+//   K1 k_bc6h_quant   lane / (block, pattern): optQuantAnD_f per subset;
+//   K2 k_bc6h_shake   wave / (block, two-region shape, subset): ep_shaker_HD;
+//   K3 k_bc6h_final   lane / (block, pattern): the shaker's result where it is
+//                     better, clampF16Max, the pattern's CalcShapeError.
+struct QuantState {     // optQuantAnD_f's results for one (block, pattern)
+    float err;          // summed over the subsets in subset order
+    float pad;
+    uint64_t idx;       // indices of both subsets, 4 bits per texel
+    float ep[2][2][3];  // GetEndPoints per subset
+};
+
+__global__ void __launch_bounds__(256) k_bc6h_prep(Src src, uint32_t first, uint32_t n, int is_signed,
+                                                   float *__restrict__ din_ws)
+{
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= n) return;
+    float din[16][3];
+    load_din(src, first + b, is_signed, din);
+    float *o = din_ws + (size_t)b * 48;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) o[i * 3 + c] = din[i][c];
+}
+
+__device__ __forceinline__ void read_din(const float *__restrict__ din_ws, uint32_t b, float din[16][3])
+{
+    const float4 *p = reinterpret_cast<const float4 *>(din_ws + (size_t)b * 48);
+    float v[48];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const float4 w = p[k];
+        v[4 * k] = w.x;
+        v[4 * k + 1] = w.y;
+        v[4 * k + 2] = w.z;
+        v[4 * k + 3] = w.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) din[i][c] = v[i * 3 + c];
+}
+
+__global__ void __launch_bounds__(256) k_bc6h_quant(uint32_t n, const float *__restrict__ din_ws,
+                                                    QuantState *__restrict__ qs)
 {
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t b = gid / kPatterns;
     const int pat = (int)(gid % kPatterns);
     if (b >= n) return;
     float din[16][3];
-    load_din(src, first + b, is_signed, din);
+    read_din(din_ws, b, din);
     const int shape = pat - 1;
     const int ns = shape >= 0 ? 2 : 1, ncl = shape >= 0 ? 8 : 16;
     float dir[3] = {0.f, 0.f, 0.f};
-    float err0 = 0.0f;
-    float ep[2][2][3] = {};
+    QuantState q;
+    q.err = 0.0f;
+    q.pad = 0.0f;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) q.ep[s][e][c] = 0.f;
     int qidx[16];
     uint64_t idx0 = 0;
-    uint32_t masks[2] = {subset_mask(shape, 0), subset_mask(shape, 1)};
+    const uint32_t masks[2] = {subset_mask(shape, 0), subset_mask(shape, 1)};
     for (int s = 0; s < ns; ++s) {
-        err0 += opt_quant_f(din, masks[s], ncl, qidx, dir, ep[s]);
+        q.err += opt_quant_f(din, masks[s], ncl, qidx, dir, q.ep[s]);
 #pragma unroll
         for (int k = 0; k < 16; ++k)
             if ((masks[s] >> k) & 1u) idx0 = set_nib(idx0, k, qidx[k]);
     }
+    q.idx = idx0;
+    qs[(size_t)b * kPatterns + pat] = q;
+}
+
+// USE_SHAKERHD at quality 1.0 > 0.80 (:960-1025): every two-region shape's
+// subsets are shaken from the quantiser's indices
+__global__ void __launch_bounds__(256) k_bc6h_shake(uint32_t n, const float *__restrict__ din_ws,
+                                                    const QuantState *__restrict__ qs, ShakeOut *__restrict__ so)
+{
+    // wave-uniform by construction; readfirstlane lets the compiler see it
+    const uint32_t wid = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const uint32_t b = wid >> 6;
+    const int shape = (int)((wid >> 1) & 31u), sub = (int)(wid & 1u);
+    if (b >= n) return;   // whole waves
+    const int L = (int)__lane_id();
+    float x[3] = {0.f, 0.f, 0.f};
+    if (L < 16)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) x[c] = din_ws[(size_t)b * 48 + L * 3 + c];
+    const uint64_t qi = qs[(size_t)b * kPatterns + 1 + shape].idx;
+    const int idxt = L < 16 ? nib(qi, L) : 0;
+    const uint32_t mask = subset_mask(shape, sub);
+    const int nm = __popc(mask);
+    ShakeOut out;
+    if (nm >= 8)
+        shake_hd_wave<3>(x, idxt, mask, out);
+    else if (nm >= 4)
+        shake_hd_wave<2>(x, idxt, mask, out);
+    else if (nm >= 2)
+        shake_hd_wave<1>(x, idxt, mask, out);
+    else
+        shake_hd_wave<0>(x, idxt, mask, out);
+    if (L == 0) so[((size_t)b * 32 + shape) * 2 + sub] = out;
+}
+
+__global__ void __launch_bounds__(256) k_bc6h_final(uint32_t n, int is_signed, const float *__restrict__ din_ws,
+                                                    const QuantState *__restrict__ qs, const ShakeOut *__restrict__ so,
+                                                    PatternState *__restrict__ ws)
+{
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t b = gid / kPatterns;
+    const int pat = (int)(gid % kPatterns);
+    if (b >= n) return;
+    const QuantState q = qs[(size_t)b * kPatterns + pat];
+    const int shape = pat - 1;
+    const int ns = shape >= 0 ? 2 : 1;
     PatternState st;
     st.pad = 0.f;
-    uint64_t idx = idx0;
+    uint64_t idx = q.idx;
     bool shaker = false;
     int epo[2][2][3] = {};
-    if (shape >= 0) {   // USE_SHAKERHD, quality 1.0 > 0.80 (:960-1025)
+    if (shape >= 0) {
+        const ShakeOut s0 = so[((size_t)b * 32 + shape) * 2], s1 = so[((size_t)b * 32 + shape) * 2 + 1];
         float err1 = 0.0f;
-        uint64_t idx1 = 0;
-        for (int s = 0; s < 2; ++s) {
-            int tmp[16];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) tmp[k] = nib(idx0, k);
-            err1 += shaker_dispatch(din, masks[s], tmp, epo[s]);
-#pragma unroll
-            for (int k = 0; k < 16; ++k)
-                if ((masks[s] >> k) & 1u) idx1 = set_nib(idx1, k, tmp[k]);
-        }
-        if (err0 > err1) {
+        err1 += s0.err;
+        err1 += s1.err;
+        if (q.err > err1) {
             shaker = true;
-            idx = idx1;
+            idx = s0.idx | s1.idx;   // disjoint member nibbles
         }
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                epo[0][e][c] = s0.epo[e][c];
+                epo[1][e][c] = s1.epo[e][c];
+            }
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -851,12 +966,14 @@ __global__ void __launch_bounds__(256) k_bc6h_pattern(Src src, uint32_t first, u
 #pragma unroll
             for (int c = 0; c < 3; ++c)
                 st.fep[(s * 2 + e) * 3 + c] =
-                    clamp_f16(shaker && s < ns ? (float)epo[s][e][c] : ep[s][e][c], is_signed);
+                    clamp_f16(shaker && s < ns ? (float)epo[s][e][c] : q.ep[s][e][c], is_signed);
     st.idx = idx;
+    float din[16][3];
+    read_din(din_ws, b, din);
     float pal[16][3];
     if (shape >= 0) {
         palette<2>(st.fep, pal);
-        st.err = shape_error<2>(din, masks[1], pal);
+        st.err = shape_error<2>(din, subset_mask(shape, 1), pal);
     } else {
         palette<1>(st.fep, pal);
         st.err = shape_error<1>(din, 0u, pal);
@@ -1129,7 +1246,8 @@ __device__ __forceinline__ uint64_t reindex(const float din[16][3], const float 
 __constant__ uint32_t kRedBlock[4] = {0x00007bc2u, 0x00000000u, 0x0003e000u, 0x00000000u};
 
 // K2: pattern selection (:1593-1632), EncodePattern (:1351-1488), SaveDataBlock
-__global__ void __launch_bounds__(256) k_bc6h_encode(Src src, uint32_t first, uint32_t n, int is_signed,
+__global__ void __launch_bounds__(256) k_bc6h_encode(uint32_t first, uint32_t n, int is_signed,
+                                                     const float *__restrict__ din_ws,
                                                      const PatternState *__restrict__ ws, uint4 *__restrict__ dst,
                                                      double *__restrict__ err_out)
 {
@@ -1148,7 +1266,7 @@ __global__ void __launch_bounds__(256) k_bc6h_encode(Src src, uint32_t first, ui
     const int shape = best >= 0 ? best : 31;   // nothing restored when the one-region pattern wins
     const PatternState st = pst[1 + shape];
     float din[16][3];
-    load_din(src, first + b, is_signed, din);
+    read_din(din_ws, b, din);
     const uint32_t m1 = subset_mask(shape, 1);
     float error = best_err, best_e = 3.402823466e+38f;
     int best_fit = 0, numfits = 0;
@@ -1241,24 +1359,38 @@ static hipError_t bc6h_run(const float *blocks, const Geometry *g, uint32_t n, i
         if (e != hipSuccess) return e;
     }
     const uint32_t chunk = n < kChunk ? n : kChunk;
-    PatternState *ws = nullptr;
-    hipError_t e = hipMallocAsync((void **)&ws, (size_t)chunk * kPatterns * sizeof(PatternState), s);
+    // one allocation: din, quantiser states, shaker outputs, pattern states
+    const size_t sz_din = ((size_t)chunk * 48 * sizeof(float) + 255) & ~(size_t)255;
+    const size_t sz_q = ((size_t)chunk * kPatterns * sizeof(QuantState) + 255) & ~(size_t)255;
+    const size_t sz_s = ((size_t)chunk * 64 * sizeof(ShakeOut) + 255) & ~(size_t)255;
+    const size_t sz_p = (size_t)chunk * kPatterns * sizeof(PatternState);
+    char *mem = nullptr;
+    hipError_t e = hipMallocAsync((void **)&mem, sz_din + sz_q + sz_s + sz_p, s);
     if (e != hipSuccess) return e;
+    float *din = (float *)mem;
+    QuantState *qs = (QuantState *)(mem + sz_din);
+    ShakeOut *so = (ShakeOut *)(mem + sz_din + sz_q);
+    PatternState *ws = (PatternState *)(mem + sz_din + sz_q + sz_s);
     Src src;
     src.blocks = blocks;
     if (g) src.g = *g;
     src.force_alpha_one = force_alpha_one;
     for (uint32_t first = 0; first < n; first += chunk) {
         const uint32_t m = (n - first) < chunk ? (n - first) : chunk;
-        const uint64_t nl = (uint64_t)m * kPatterns;
-        hipLaunchKernelGGL(k_bc6h_pattern, dim3((uint32_t)((nl + 255) / 256)), dim3(256), 0, s, src, first, m,
-                           is_signed, ws);
-        hipLaunchKernelGGL(k_bc6h_encode, dim3((m + 255) / 256), dim3(256), 0, s, src, first, m, is_signed,
-                           (const PatternState *)ws, (uint4 *)dst, err);
+        const uint64_t nl = (uint64_t)m * kPatterns, nw = (uint64_t)m * 64 * 64;
+        hipLaunchKernelGGL(k_bc6h_prep, dim3((m + 255) / 256), dim3(256), 0, s, src, first, m, is_signed, din);
+        hipLaunchKernelGGL(k_bc6h_quant, dim3((uint32_t)((nl + 255) / 256)), dim3(256), 0, s, m, (const float *)din,
+                           qs);
+        hipLaunchKernelGGL(k_bc6h_shake, dim3((uint32_t)((nw + 255) / 256)), dim3(256), 0, s, m, (const float *)din,
+                           (const QuantState *)qs, so);
+        hipLaunchKernelGGL(k_bc6h_final, dim3((uint32_t)((nl + 255) / 256)), dim3(256), 0, s, m, is_signed,
+                           (const float *)din, (const QuantState *)qs, (const ShakeOut *)so, ws);
+        hipLaunchKernelGGL(k_bc6h_encode, dim3((m + 255) / 256), dim3(256), 0, s, first, m, is_signed,
+                           (const float *)din, (const PatternState *)ws, (uint4 *)dst, err);
         e = hipGetLastError();
         if (e != hipSuccess) break;
     }
-    const hipError_t ef = hipFreeAsync(ws, s);
+    const hipError_t ef = hipFreeAsync(mem, s);
     return e != hipSuccess ? e : ef;
 }
 

@@ -26,7 +26,8 @@ def build():
     o = os.path.join(ROOT, "oracle")
     subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-pthread", "-std=gnu11",
                     "-DORC_TRACE", "-shared", "-o", SO, os.path.join(ROOT, "tools", "prune_study.c"),
-                    os.path.join(o, "orc_bc7.c"), os.path.join(o, "orc_bcx.c"), os.path.join(o, "orc_image.c"),
+                    os.path.join(o, "orc_bc7.c"), os.path.join(o, "orc_bcx.c"), os.path.join(o, "orc_image.c"), os.path.join(o, "orc_bc7enc.c"),
+                    os.path.join(o, "orc_bc6h.c"),
                     "-lm", "-I", o], check=True)
 
 
