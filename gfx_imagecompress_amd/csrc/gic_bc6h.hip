@@ -581,26 +581,40 @@ __device__ void shake_hd_wave(const float x[3], int idxt, uint32_t mask, ShakeOu
 #pragma unroll
                 for (int j = 0; j < 3; ++j) cc[j] = floorf(sm[j] / (float)cnt + 0.5f);
         }
+        // The least-squares sums of an expansion ck = c0 * q + p are float sums of
+        // integers below 2^24 in magnitude (|cc| <= 0x7c00, Mi_ <= 15, <= 16
+        // members), so every partial sum is exact and they equal integer
+        // polynomials in (q, p) over the subset's moments N, S1 = sum c0,
+        // S2 = sum c0^2, C0 = sum cc, C1 = sum c0 * cc.
+        int S1 = 0, S2 = 0, C0[3] = {0, 0, 0}, C1[3] = {0, 0, 0};
+        for (uint32_t mm = mask; mm; mm &= mm - 1) {
+            const int u = __builtin_ctz(mm);
+            const int cu = rbi(c0, u);
+            S1 += cu;
+            S2 += cu * cu;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const int c = (int)rbf(cc[j], u);
+                C0[j] += c;
+                C1[j] += cu * c;
+            }
+        }
         const int s = L ^ (L >> 1);   // the walk's state after step p1 = L
         float err_2 = 3.402823466e+38f;
         uint64_t idx_2 = 0;
         int epo_2[2][3] = {{0, 0, 0}, {0, 0, 0}};
         for (int q = 1; q * Mi <= Mi_; q++)
             for (int p = 0; p <= Mi_ - q * Mi; p++) {
-                // least squares on the rounded cluster means (:2377-2437), member order
-                float im00 = 0, im01 = 0, im11 = 0, rp[2][3] = {{0, 0, 0}, {0, 0, 0}};
-                for (uint32_t mm = mask; mm; mm &= mm - 1) {
-                    const int u = __builtin_ctz(mm);
-                    const int ck = rbi(c0, u) * q + p;
-                    im00 += (float)((Mi_ - ck) * (Mi_ - ck));
-                    im01 += (float)(ck * (Mi_ - ck));
-                    im11 += (float)(ck * ck);
+                // least squares on the rounded cluster means (:2377-2437)
+                const int sc = q * S1 + p * n, sc2 = q * q * S2 + 2 * p * q * S1 + p * p * n;
+                const float im00 = (float)(Mi_ * Mi_ * n - 2 * Mi_ * sc + sc2), im01 = (float)(Mi_ * sc - sc2),
+                            im11 = (float)sc2;
+                float rp[2][3];
 #pragma unroll
-                    for (int j = 0; j < 3; ++j) {
-                        const float c = rbf(cc[j], u);
-                        rp[0][j] += (float)(Mi_ - ck) * c;
-                        rp[1][j] += (float)ck * c;
-                    }
+                for (int j = 0; j < 3; ++j) {
+                    const int r1 = q * C1[j] + p * C0[j];
+                    rp[0][j] = (float)(Mi_ * C0[j] - r1);
+                    rp[1][j] = (float)r1;
                 }
                 const float dd = im00 * im11 - im01 * im01;
                 const float i10 = im00;
