@@ -646,9 +646,19 @@ __device__ void shake_hd_wave(const float x[3], int idxt, uint32_t mask, ShakeOu
 #pragma unroll
                     for (int c = 0; c < NCL; ++c) R[j][c] = ramp8<CLOG>(a, b, c);
                 }
+                // Exact cut: the partial sums only grow (non-negative terms), so once
+                // every corner's partial error has reached err_2 this expansion
+                // cannot change the outcome (it needs err_1 < err_2) and its walk
+                // is abandoned.
                 float err_0 = 0;
                 uint64_t idx_0 = 0;
-                for (uint32_t mm = mask; mm; mm &= mm - 1) {
+                bool cut = false;
+                int k = 0;
+                for (uint32_t mm = mask; mm; mm &= mm - 1, ++k) {
+                    if ((k & 1) == 0 && k && __all(err_0 >= err_2)) {
+                        cut = true;
+                        break;
+                    }
                     const int i = __builtin_ctz(mm);
                     const float d0 = rbf(x[0], i), d1 = rbf(x[1], i), d2 = rbf(x[2], i);
                     int ci = 0;
@@ -668,6 +678,7 @@ __device__ void shake_hd_wave(const float x[3], int idxt, uint32_t mask, ShakeOu
                     idx_0 |= (uint64_t)ci << (4 * i);
                     err_0 += cmin;
                 }
+                if (cut) continue;
                 int w;
                 const float err_1 = wave_first_min(err_0, w);
                 if (err_1 < err_2) {
