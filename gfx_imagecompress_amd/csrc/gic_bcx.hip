@@ -116,6 +116,34 @@ struct ColF {
     __device__ __forceinline__ float rpt(int i) const { return r[i]; }
     __device__ __forceinline__ float blk(int i, int ch) const { return cc[i][ch] / 255.f; }
 };
+// ColB's words parked in LDS through the endpoint search (colour i of a lane at
+// w[i * kLdsStride], lane-contiguous rows, so a wave's reads are conflict-free):
+// the search loop needs only the projections, and 16 colour words held in
+// VGPRs across it pushed the kernel past 3 waves/SIMD into scratch.  Volatile:
+// every use re-reads, nothing is hoisted into registers.  Refine takes a
+// register copy (regs()).
+constexpr int kLdsStride = 256;
+struct ColL {
+    volatile uint32_t *w;
+    int n;
+    const volatile float *lut;
+    __device__ __forceinline__ uint32_t word(int i) const { return w[i * kLdsStride]; }
+    __device__ __forceinline__ float c(int i, int ch) const { return ubyte_f(word(i), ch); }
+    __device__ __forceinline__ float rpt(int i) const { return ubyte_f(word(i), 3); }
+    __device__ __forceinline__ float blk(int i, int ch) const { return lut[(word(i) >> (8 * ch)) & 255u]; }
+    __device__ __forceinline__ ColB regs() const
+    {
+        ColB r;
+        r.lut = lut;
+        r.n = n;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) r.u[i] = word(i);
+        return r;
+    }
+};
+__device__ __forceinline__ const ColB &regs(const ColB &u) { return u; }
+__device__ __forceinline__ const ColF &regs(const ColF &u) { return u; }
+__device__ __forceinline__ ColB regs(const ColL &u) { return u.regs(); }
 
 // ClstrErr (weighted), amd_bcx_body.cpp:214-255
 template <int N, class Col>
@@ -576,10 +604,11 @@ __device__ __forceinline__ void fit_endpoints(float result[3][2], const Col &u, 
             for (int j = 0; j < 3; ++j) rc[j][k] = (pos_g[k] * dir_g[j] + mid[j]) * 255.f;
     }
     snap_grid(result, rc);
+    const auto &ur = regs(u);
     if (R3D)
-        refine_3d<N>(result, u, steps);
+        refine_3d<N>(result, ur, steps);
     else
-        refine_channels<N>(result, u, steps);
+        refine_channels<N>(result, ur, steps);
 }
 
 // Leaders and ranks of the kept texels' colour keys: a kept texel leads its
@@ -870,6 +899,26 @@ __device__ __forceinline__ uint2 encode_bc1_u8(const uint32_t px[16], int steps,
     int kept;
     unique_colours(u, px, use_alpha, thr_keep, kept);
     return encode_bc1<R3D>(u, kept, t, steps, use_alpha);
+}
+
+// the same with the colour words parked in LDS (ColL; w = this lane's column)
+template <bool R3D>
+__device__ __forceinline__ uint2 encode_bc1_u8_lds(const uint32_t px[16], int steps, bool use_alpha, uint32_t thr_keep,
+                                                   const TexG &t, const volatile float *lut, volatile uint32_t *w)
+{
+    int kept;
+    ColL ul;
+    {
+        ColB u;
+        u.lut = lut;
+        unique_colours(u, px, use_alpha, thr_keep, kept);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i * kLdsStride] = u.u[i];
+        ul.n = u.n;
+    }
+    ul.w = w;
+    ul.lut = lut;
+    return encode_bc1<R3D>(ul, kept, t, steps, use_alpha);
 }
 
 template <bool R3D>
@@ -1176,6 +1225,7 @@ template <bool R3D>
 __global__ void __launch_bounds__(256, 3) bc1_image_kernel(Geometry g, Bc1Params p, uint2 *__restrict__ dst)
 {
     __shared__ float lut[256];   // byte -> v / 255.0f
+    __shared__ uint32_t cols[16 * bcx::kLdsStride];   // ColL words of the workgroup's lanes
     lut[threadIdx.x] = (float)threadIdx.x / 255.0f;
     __syncthreads();
     const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1185,7 +1235,7 @@ __global__ void __launch_bounds__(256, 3) bc1_image_kernel(Geometry g, Bc1Params
     uint32_t px[16];
     load_block_u8(g, slice, by, bx, p.force_alpha_one != 0, px);
     const bcx::TexG t{g, slice, by, bx, p.force_alpha_one != 0, p.thr_final};
-    dst[id] = bcx::encode_bc1_u8<R3D>(px, p.steps, p.alpha_threshold > 0.0f, p.thr_keep, t, lut);
+    dst[id] = bcx::encode_bc1_u8_lds<R3D>(px, p.steps, p.alpha_threshold > 0.0f, p.thr_keep, t, lut, cols + threadIdx.x);
 }
 
 // BC2 / BC3 (amd_bc2_compressor.cpp:36-50, amd_bc3_compressor.cpp:36-50): alpha
