@@ -763,7 +763,7 @@ struct TexV {
 // source address is made opaque so the compiler cannot reuse the first load).
 struct TexG {
     Geometry g;
-    uint32_t slice, by, bx;
+    uint32_t id;   // the block; its coordinates are recomputed (one VGPR live, not three)
     bool force_alpha_one;
     uint32_t thr_final;
     __device__ __forceinline__ TexV view() const
@@ -772,6 +772,8 @@ struct TexG {
         const uint8_t *src = gg.src;
         asm volatile("" : "+s"(src));
         gg.src = src;
+        uint32_t slice, by, bx;
+        block_coords(gg, id, slice, by, bx);
         TexV v;
         v.thr_final = thr_final;
         load_block_u8(gg, slice, by, bx, force_alpha_one, v.px);
@@ -861,22 +863,10 @@ __device__ __forceinline__ float comp_rgba(const Tex &t, int steps, bool use_alp
     return err;
 }
 
-// Image_CompressAMDBC1Block, amd_bcx_helpers.cpp:51-105
-template <bool R3D, class Col, class Tex>
-__device__ __forceinline__ uint2 encode_bc1(const Col &u, int kept, const Tex &t, int steps, bool use_alpha)
+// BC1 block words of one ramp's result: colours as 565, swapped so the block
+// decodes in the 4-colour (c0 > c1) or 3-colour (c0 <= c1) mode
+__device__ __forceinline__ uint2 pack_bc1(const uint8_t ep[3][2], uint32_t ibits, bool m4)
 {
-    uint8_t ep3[3][2], ep4[3][2];
-    uint32_t i3 = 0, i4 = 0;
-    const double e3 = comp_rgba<3, R3D>(t, steps, use_alpha, ep3, i3, u, kept);
-    double e4 = 3.402823466e+38;
-    if (!(e3 == 0.0)) e4 = comp_rgba<4, R3D>(t, steps, use_alpha, ep4, i4, u, kept);
-    const bool m4 = !(e3 <= e4);
-    uint8_t ep[3][2];
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-        ep[ch][0] = m4 ? ep4[ch][0] : ep3[ch][0];
-        ep[ch][1] = m4 ? ep4[ch][1] : ep3[ch][1];
-    }
     const unsigned c0 = ((unsigned)(ep[CH_R][0] >> 3) << 11) | ((unsigned)(ep[CH_G][0] >> 2) << 5) |
                         (unsigned)(ep[CH_B][0] >> 3);
     const unsigned c1 = ((unsigned)(ep[CH_R][1] >> 3) << 11) | ((unsigned)(ep[CH_G][1] >> 2) << 5) |
@@ -886,8 +876,31 @@ __device__ __forceinline__ uint2 encode_bc1(const Col &u, int kept, const Tex &t
         out.x = c1 | (c0 << 16);
     else
         out.x = c0 | (c1 << 16);
-    out.y = m4 ? i4 : i3;
+    out.y = ibits;
     return out;
+}
+
+// Image_CompressAMDBC1Block, amd_bcx_helpers.cpp:51-105.  The 3-colour result is
+// packed into its block words before the 4-colour search runs, so only those two
+// words and its error stay live across it.
+template <bool R3D, class Col, class Tex>
+__device__ __forceinline__ uint2 encode_bc1(const Col &u, int kept, const Tex &t, int steps, bool use_alpha)
+{
+    uint2 b3;
+    float e3f;
+    {
+        uint8_t ep3[3][2];
+        uint32_t i3 = 0;
+        e3f = comp_rgba<3, R3D>(t, steps, use_alpha, ep3, i3, u, kept);
+        b3 = pack_bc1(ep3, i3, false);
+    }
+    const double e3 = e3f;
+    if (e3 == 0.0) return b3;
+    uint8_t ep4[3][2];
+    uint32_t i4 = 0;
+    const double e4 = comp_rgba<4, R3D>(t, steps, use_alpha, ep4, i4, u, kept);
+    const bool m4 = !(e3 <= e4);
+    return m4 ? pack_bc1(ep4, i4, true) : b3;
 }
 
 template <bool R3D>
@@ -1234,7 +1247,7 @@ __global__ void __launch_bounds__(256, 3) bc1_image_kernel(Geometry g, Bc1Params
     block_coords(g, id, slice, by, bx);
     uint32_t px[16];
     load_block_u8(g, slice, by, bx, p.force_alpha_one != 0, px);
-    const bcx::TexG t{g, slice, by, bx, p.force_alpha_one != 0, p.thr_final};
+    const bcx::TexG t{g, id, p.force_alpha_one != 0, p.thr_final};
     dst[id] = bcx::encode_bc1_u8_lds<R3D>(px, p.steps, p.alpha_threshold > 0.0f, p.thr_keep, t, lut, cols + threadIdx.x);
 }
 
