@@ -861,21 +861,29 @@ extern "C" int gic_save_dds(Image_ImageHeader const *img, const char *path)
 
 // ---- block level: one-block GPU launches (prefer gic_hip_encode_blocks_f32 for batches)
 
+static thread_local int t_block_status = GIC_OK;
+
+extern "C" int gic_block_last_status(void) { return t_block_status; }
+
 static bool encode_one_block(gic_format fmt, const float *in, size_t nfloats, const gic_options &o, void *out,
                              size_t out_bytes)
 {
     DeviceScratch &s = t_scratch;
-    bool ok = s.reserve(nfloats * sizeof(float), out_bytes) &&
-              hipMemcpyAsync(s.src, in, nfloats * sizeof(float), hipMemcpyHostToDevice, s.stream) == hipSuccess &&
-              gic_hip_encode_blocks_f32(fmt, (const float *)s.src, 1, &o, (uint8_t *)s.dst, nullptr, s.stream) ==
-                  GIC_OK &&
-              hipMemcpyAsync(out, s.dst, out_bytes, hipMemcpyDeviceToHost, s.stream) == hipSuccess &&
-              hipStreamSynchronize(s.stream) == hipSuccess;
-    if (!ok) {
-        fprintf(stderr, "gfx_imagecompress_amd: block encode failed on the GPU\n");
+    int st = GIC_OK;
+    if (!s.reserve(nfloats * sizeof(float), out_bytes) ||
+        hipMemcpyAsync(s.src, in, nfloats * sizeof(float), hipMemcpyHostToDevice, s.stream) != hipSuccess)
+        st = GIC_EHIP;
+    if (st == GIC_OK)
+        st = gic_hip_encode_blocks_f32(fmt, (const float *)s.src, 1, &o, (uint8_t *)s.dst, nullptr, s.stream);
+    if (st == GIC_OK && (hipMemcpyAsync(out, s.dst, out_bytes, hipMemcpyDeviceToHost, s.stream) != hipSuccess ||
+                         hipStreamSynchronize(s.stream) != hipSuccess))
+        st = GIC_EHIP;
+    t_block_status = st;
+    if (st != GIC_OK) {
+        fprintf(stderr, "gfx_imagecompress_amd: block encode failed (%d)\n", st);
         memset(out, 0, out_bytes);
     }
-    return ok;
+    return st == GIC_OK;
 }
 
 extern "C" void Image_CompressAMDBC1Block(float const input[64], bool adaptive, bool b3d, uint8_t steps,
@@ -963,6 +971,7 @@ extern "C" void Image_CompressRichGel999BC7enc16(uint32_t const input[16], bool 
                                              s.stream) == GIC_OK &&
                     hipMemcpyAsync(out, s.dst, 16, hipMemcpyDeviceToHost, s.stream) == hipSuccess &&
                     hipStreamSynchronize(s.stream) == hipSuccess;
+    t_block_status = ok ? GIC_OK : GIC_EHIP;
     if (!ok) {
         fprintf(stderr, "gfx_imagecompress_amd: block encode failed on the GPU\n");
         memset(out, 0, 16);

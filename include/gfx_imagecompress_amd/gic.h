@@ -173,6 +173,12 @@ int gic_save_dds(struct Image_ImageHeader const *img, const char *path);
 /* Last HIP error code recorded by this thread (0 if none). */
 int gic_last_hip_error(void);
 
+/* Status of this thread's last block-level call (Image_CompressAMD*Block,
+ * Image_CompressRichGel999BC7enc16): GIC_OK, or the gic_* code of the failure.
+ * Those entry points return void as in the reference (imagecompress.h:111-141);
+ * a failed one writes a zero block, prints to stderr and sets this status. */
+int gic_block_last_status(void);
+
 /* Library version string. */
 const char *gic_version(void);
 

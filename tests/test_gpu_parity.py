@@ -122,6 +122,24 @@ def test_bc1_block_api_arbitrary_floats(gpu):
         assert out4.tobytes() == oracle_lib.bc4_block(v), k
 
 
+def test_block_api_status(gpu):
+    """The void block entry points report their outcome through
+    gic_block_last_status(): 0 after a good call; adaptive colour weights (UB in
+    the reference, not implemented) give GIC_EUNSUP and a zero block."""
+    lib = gic.library()
+    lib.gic_block_last_status.restype = ctypes.c_int
+    blk = np.random.default_rng(9).random((16, 4), dtype=np.float32)
+    out = np.full(8, 0xAB, np.uint8)
+    lib.Image_CompressAMDBC1Block(blk.ctypes.data_as(ctypes.c_void_p), False, False, 1,
+                                  ctypes.c_float(0.0), out.ctypes.data_as(ctypes.c_void_p))
+    assert lib.gic_block_last_status() == gic.GIC_OK
+    assert out.tobytes() == oracle_lib.bc1_block(blk, threshold=0.0)
+    lib.Image_CompressAMDBC1Block(blk.ctypes.data_as(ctypes.c_void_p), True, False, 1,
+                                  ctypes.c_float(0.0), out.ctypes.data_as(ctypes.c_void_p))
+    assert lib.gic_block_last_status() == gic.GIC_EUNSUP
+    assert not out.any()
+
+
 def test_bc1_refinement_steps_option(gpu):
     img = synth.g1(64, 64)
     for steps in (0, 2, 3):
