@@ -18,6 +18,7 @@
 // and "first strictly smaller" selection is unchanged.
 
 #include "gic_common.h"
+#include "gic_fastdiv.h"
 
 namespace gic {
 namespace bcx {
@@ -67,6 +68,14 @@ __device__ __forceinline__ bool expand_grid(float out[3][2], const float in[3][2
 }
 
 // BldClrRmp, amd_bcx_body.cpp:188-197 (n is 3 or 4)
+// (x / (N - 1) is the IEEE quotient either way: N = 3 halves exactly, N = 4 takes
+// div3_rn, gic_fastdiv.h)
+template <int N>
+__device__ __forceinline__ float div_nm1(float x)
+{
+    return N == 4 ? div3_rn(x) : x / (float)(N - 1);
+}
+
 template <int N>
 __device__ __forceinline__ void chan_ramp(float r[4], const float ends[2])
 {
@@ -76,7 +85,7 @@ __device__ __forceinline__ void chan_ramp(float r[4], const float ends[2])
     if (N & 1) r[N] = 1000000.f;
 #pragma unroll
     for (int e = 1; e < N - 1; ++e)
-        r[e] = floorf((r[0] * (float)(N - 1 - e) + r[N - 1] * (float)e + rnd) / (float)(N - 1));
+        r[e] = floorf(div_nm1<N>(r[0] * (float)(N - 1 - e) + r[N - 1] * (float)e + rnd));
 }
 
 // Unique colours of a block (B,G,R x255 as floats, sorted as QSortFloatCmp)
@@ -348,9 +357,9 @@ __device__ __forceinline__ RampStep ramp_step(float lo, float hi)
     RampStep r;
     r.lo = lo;
     r.hi = hi;
-    r.step = (hi - lo) / (float)(N - 1);
+    r.step = div_nm1<N>(hi - lo);
     r.step_h = r.step * (float)0.5;
-    r.rstep = (float)1.0f / r.step;
+    r.rstep = rcp_rn(r.step);
     return r;
 }
 
@@ -559,9 +568,9 @@ __device__ __forceinline__ void fit_endpoints(float result[3][2], const Col &u, 
             dir_g[2] = dir[2];
             pos_g[0] = pos0;
             pos_g[1] = pos1;
-            const float step = (pos1 - pos0) / (float)(N - 1);
+            const float step = div_nm1<N>(pos1 - pos0);
             const float step_h = step * (float)0.5;
-            const float rstep = (float)1.0f / step;
+            const float rstep = rcp_rn(step);
             const float over_n = 1.f / (float)(N - 1);
             const float avg = (float)(N - 1) / 2.f;
             float crs[3] = {0, 0, 0}, len = 0.f;
