@@ -3,6 +3,14 @@
 // both over every float input on the GPU, log in profiles/).
 #pragma once
 
+// GIC_FASTDIV_HOST: div3_rn as a host function (tests/fastdiv_check.cpp); rcp_rn
+// needs v_rcp_f32 and is device-only
+#ifdef GIC_FASTDIV_HOST
+#define GIC_FD inline
+#else
+#define GIC_FD __device__ __forceinline__
+#endif
+
 namespace gic {
 
 // RN(d / 3): q0 = d * RN(1/3), r = d - 3 q0 exactly (FMA), q = q0 + r * RN(1/3);
@@ -10,7 +18,7 @@ namespace gic {
 // (the check's only mismatches are d = +-inf, which the BC1 search never
 // divides: its dividends are differences and sums of bounded projections and
 // colour values)
-__device__ __forceinline__ float div3_rn(float d)
+GIC_FD float div3_rn(float d)
 {
     const float C = 0x1.555556p-2f;
     const float q0 = d * C;
@@ -18,6 +26,7 @@ __device__ __forceinline__ float div3_rn(float d)
     return __builtin_copysignf(__builtin_fmaf(r, C, q0), d);
 }
 
+#ifndef GIC_FASTDIV_HOST
 // RN(1 / s) for normal s away from the range ends: v_rcp_f32 (1 ulp) and one
 // FMA Newton step; zero, denormal, huge and non-finite s take the IEEE sequence
 __device__ __forceinline__ float rcp_rn(float s)
@@ -28,5 +37,6 @@ __device__ __forceinline__ float rcp_rn(float s)
     const float e = __builtin_fmaf(-s, r0, 1.0f);
     return __builtin_fmaf(e, r0, r0);
 }
+#endif
 
 }  // namespace gic
