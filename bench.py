@@ -85,6 +85,9 @@ def parse():
                         "the ranks (strong scaling) and one timed RCCL gather to rank 0")
     p.add_argument("--batch-slices", type=int, default=64)
     p.add_argument("--batch-size", type=int, default=4096)
+    p.add_argument("--no-batch", action="store_true",
+                   help="8k workload: skip the configs[4] legs (64 x 4096^2 BC7 batch: bounded exit and exact search)")
+    p.add_argument("--no-batch-exact", action="store_true", help="8k workload: skip the exact-search configs[4] leg")
     p.add_argument("--shard-chunk", type=int, default=16,
                    help="batch64: block rows per chunk dealt round-robin over the ranks (0 = one contiguous "
                         "range per rank)")
@@ -237,6 +240,7 @@ def bc7_secondary(args, gic, src, size, avail_rows, world, dev, rank, shake_rank
         dist.barrier()
     torch.cuda.synchronize(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    gic.iter_cap_hits(reset=True)
     t0 = time.perf_counter()
     ev0.record(stream)
     gic.encode_device(7, src, size, size, 1, 4, dst, opts, 0, rows, stream=stream)
@@ -250,6 +254,7 @@ def bc7_secondary(args, gic, src, size, avail_rows, world, dev, rank, shake_rank
     t = _max_over_ranks(torch.tensor([wall, own], dtype=torch.float64, device=dev), world)
     wall, kern_ms = float(t[0]), float(t[1])
     spread = _spread_over_ranks(own, world)
+    hits = gic.iter_cap_hits(reset=True)
     px = size * rows * 4 * world
     search = "exact (reference search, bit-identical)" if shake_ranks == 0 else \
         f"pruned: {shake_ranks} partitions shaken per mode (per-block MSE tolerance)"
@@ -261,7 +266,7 @@ def bc7_secondary(args, gic, src, size, avail_rows, world, dev, rank, shake_rank
            "value": round(px / wall / 1e6, 4), "unit": "Mpixels/s",
            "blocks_per_s": round(bx * rows * world / wall, 1), "ms_per_pass": round(wall * 1e3, 2),
            "kernel_ms": round(kern_ms, 2), "kernel_ms_rank_min_max": [round(x, 2) for x in spread],
-           "rows_per_gpu": rows * 4, "dtype": "f64+int32",
+           "rows_per_gpu": rows * 4, "dtype": "f64+int32", "iter_cap_hits": hits,
            "roofline": {"bound": "valu", "alg_bytes_per_launch": 80 * bx * rows,
                         "hbm_frac": round(80 * bx * rows / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 8)}}
     if rank == 0 and not args.no_cpu and ref_rows is not None:
@@ -428,55 +433,70 @@ def bc7enc16_leg(args, gic, src, size, world, dev, rank, fast):
     return res
 
 
-def bc6h_leg(args, gic, world, dev, rank):
-    """BC6H (unsigned half floats, BC6HBlockEncoder at the
-    image API's quality 1.0) on a synthetic HDR float32 texture (synth.hdr_rgba:
-    12 stops, noise, highlights), steps x one launch over the rank's texture,
-    plus (rank 0) the CPU restatement on a bounded sample of blocks with a
+def bc6h_leg(args, gic, world, dev, rank, signed=False):
+    """SURVEY.md 8(f)4: BC6H (BC6HBlockEncoder at the image API's quality 1.0;
+    unsigned half floats, or signed for a signed source) on a synthetic HDR
+    float32 texture (synth.hdr_rgba: 12 stops, noise, highlights; signed: a
+    sign from a hash), steps x one launch over the rank's texture, plus (rank
+    0) the CPU restatement on a bounded sample of whole blocks with a
     bit-exactness check."""
     import numpy as np
     import torch
     from gfx_imagecompress_amd import synth
     n = args.bc6h_size
     bx = by = (n + 3) // 4
-    img = synth.hdr_rgba(n, n, seed=1 + rank)
+    img = synth.hdr_rgba(n, n, seed=1 + rank, signed=signed)
     src = torch.from_numpy(img.reshape(-1).copy()).to(dev)
     dst = torch.empty(bx * by * 16, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
+    fmt = gic.FMT_BC6H_SF if signed else gic.FMT_BC6H
 
     def step():
-        gic.encode_device_src(gic.FMT_BC6H, gic.SRC_FLOAT32, src, n, n, 1, 4, dst, stream=stream)
+        gic.encode_device_src(fmt, gic.SRC_FLOAT32, src, n, n, 1, 4, dst, stream=stream)
     step()
-    wall, kern_ms = _timed(world, dev, stream, step, max(1, min(args.steps, 3)))
     steps = max(1, min(args.steps, 3))
-    res = {"metric": f"Mpixels/s BC6H (unsigned, quality 1.0) on a {n}x{n} synthetic HDR float32 texture",
+    gic.iter_cap_hits(reset=True)
+    wall, kern_ms = _timed(world, dev, stream, step, steps)
+    hits = gic.iter_cap_hits(reset=True)
+    res = {"metric": f"Mpixels/s BC6H ({'signed' if signed else 'unsigned'}, quality 1.0) on a {n}x{n} synthetic "
+                     f"HDR float32 texture",
            "value": round(n * n * world * steps / wall / 1e6, 4), "unit": "Mpixels/s",
            "blocks_per_s": round(bx * by * world * steps / wall, 1), "ms_per_step": round(wall / steps * 1e3, 3),
            "kernel_ms": round(kern_ms, 3), "kernel_ms_rank_min_max": [round(x, 3) for x in _timed.spread],
-           "dtype": "f32", "steps": steps,
+           "dtype": "f32", "steps": steps, "iter_cap_hits": hits,
            "roofline": {"bound": "valu", "alg_bytes_per_launch": 272 * bx * by,
                         "hbm_frac": round(272 * bx * by / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 8),
                         "note": "272 B per block: 256 B of float32 RGBA texels read, 16 B written"}}
+    valu = _valu_roofline("valu_bc6h_shake_signed.json" if signed else "valu_bc6h_shake.json", n, n, kern_ms,
+                          launch_key="bc6h_ms")
+    if valu is not None:
+        res["roofline"]["valu"] = valu
     if rank == 0 and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib
         threads = _cpu_threads()
-        blocks = img[:16].reshape(4, 4, bx, 4, 4).transpose(0, 2, 1, 3, 4).reshape(-1, 64)   # block rows 0-3
+        # whole blocks of block rows 0-3 (the edge clamp of ReadNxNBlockF for a ragged size)
+        rows = min(by, 4)
+        ys = np.minimum(np.arange(rows * 4), n - 1)
+        xs = np.minimum(np.arange(bx * 4), n - 1)
+        t = img[ys][:, xs]
+        blocks = t.reshape(rows, 4, bx, 4, 4).transpose(0, 2, 1, 3, 4).reshape(-1, 64)
         nsamp = min(len(blocks), 1024)
         c0 = time.perf_counter()
-        ref, _ = oracle_lib.bc6h_blocks(blocks[:nsamp], threads=threads)
+        ref, _ = oracle_lib.bc6h_blocks(blocks[:nsamp], signed=signed, threads=threads)
         dt = time.perf_counter() - c0
         got = dst.cpu().numpy().reshape(-1, 16)[:nsamp]
         res["cpu_baseline"] = {"value": round(nsamp * 16 / dt / 1e6, 5), "unit": "Mpixels/s", "cores": threads,
                                "kind": "port", "cpu_model": cpu_model(),
-                               "sample": f"the first {nsamp} blocks of block row 0 ({dt:.2f} s, {threads} threads)",
+                               "sample": f"the first {nsamp} blocks of block rows 0-{rows - 1} ({dt:.2f} s, "
+                                         f"{threads} threads)",
                                "blocks_per_s": round(nsamp / dt, 1)}
         res["gpu_parity"] = "bit-exact" if np.array_equal(got, ref) else \
             f"{int((got != ref).any(axis=1).sum())} blocks differ"
     return res
 
 
-def _valu_roofline(name, size, rows, kern_ms):
+def _valu_roofline(name, size, rows, kern_ms, launch_key=None):
     """VALU issue roofline of a kernel: SQ_INSTS_VALU per launch from the
     committed PMC summary profiles/<name> (tools/valu_json.py, same workload)
     over this run's measured launch duration; None when absent or for another
@@ -487,10 +507,11 @@ def _valu_roofline(name, size, rows, kern_ms):
             vr = json.load(f)
         if vr.get("size") != size or vr.get("rows") != rows:
             return None
-        rate = vr["valu_insts_per_launch"] / (kern_ms * 1e-3)
+        insts = vr["valu_insts_per_launch"] if launch_key is None else vr["valu_insts_per_step"]
+        rate = insts / (kern_ms * 1e-3)
         return {"bound": "valu", "achieved": round(rate / 1e12, 4), "peak": round(VALU_PEAK / 1e12, 4),
                 "unit": "T wave-instr/s", "frac": round(rate / VALU_PEAK, 4),
-                "insts_per_launch": vr["valu_insts_per_launch"], "kernel": vr.get("kernel", "")[:60],
+                "insts_per_launch": insts, "kernel": vr.get("kernel", "")[:60],
                 "source": os.path.relpath(vj, ROOT)}
     except (OSError, ValueError, KeyError):
         return None
@@ -501,15 +522,44 @@ def _cpu_threads():
     return max(1, min(threads, os.cpu_count() or 1, 64))
 
 
-def batch_workload(args, gic, world, rank, dev):
+def _batch_check_rows(S, by):
+    """(slice, block row) pairs the batch legs check against the oracle: slices
+    spread over the stack, the middle row, a shard-chunk boundary row and the
+    last row."""
+    return sorted({(0, by // 2), (S // 2, max(0, min(by - 1, 16 * (by // 32) - 1))), (S - 1, by - 1)})
+
+
+def _batch_oracle(args, S, n, bx, by, cache):
+    """The exact oracle's blocks of the check rows (computed once per run,
+    shared by the exact and the bounded legs) and the CPU time they took."""
+    if "rows" in cache:
+        return cache["rows"], cache["dt"], cache["threads"]
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    from gfx_imagecompress_amd import synth
+    threads = _cpu_threads()
+    rows, dt = {}, 0.0
+    for sl, row in _batch_check_rows(S, by):
+        img = synth.g1(n, n, seed=0x9E3779B9 + sl)
+        c0 = time.perf_counter()
+        rows[(sl, row)] = (oracle_lib.encode_image_bc7(img, quality=args.bc7_quality, first_row=row, num_rows=1,
+                                                       threads=threads), img[4 * row:4 * row + 4, :bx * 4])
+        dt += time.perf_counter() - c0
+    cache.update(rows=rows, dt=dt, threads=threads)
+    return rows, dt, threads
+
+
+def batch_run(args, gic, world, rank, dev, bound, shake_ranks, steps, warmup, src=None, oracle_cache=None):
     """configs[4]: BC7 (quality 1) over a fixed stack of S G1 slices (slice s
     seeded 0x9E3779B9+s), every slice's block rows split over the ranks
     (strong scaling: the batch is fixed, each rank does 1/N) in chunks of
     --shard-chunk rows dealt round-robin (shard.row_ranges; 0 = contiguous);
     a step = the rank's gic_hip_encode_rows calls (one per range, every slice
     at once).  After the timed steps one gather (RCCL on GPUs) brings every
-    shard to rank 0, which restores the reference block order, timed
-    separately."""
+    shard to rank 0, which restores the reference block order (timed
+    separately) and checks block rows of several slices against the oracle:
+    bit-identity for the exact search, the per-block MSE contract for the
+    bounded exit.  Returns the result dict on rank 0 (None elsewhere)."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -519,10 +569,10 @@ def batch_workload(args, gic, world, rank, dev):
     chunk = args.shard_chunk
     ranges = shard.row_ranges(by, world, rank, chunk)
     nblk = shard.shard_blocks(by, bx, S, world, rank, chunk)
-    src = synth.g1_torch(n, n, S, seed=0x9E3779B9, device=dev)
+    if src is None:
+        src = synth.g1_torch(n, n, S, seed=0x9E3779B9, device=dev)
     dst = torch.empty(max(1, nblk * 16), dtype=torch.uint8, device=dev)
-    opts = gic.Options(bc7_quality=args.bc7_quality, bc7_shake_ranks=args.bc7_shake_ranks,
-                       bc7_mse_bound=args.bc7_mse_bound)
+    opts = gic.Options(bc7_quality=args.bc7_quality, bc7_shake_ranks=shake_ranks, bc7_mse_bound=bound)
     stream = torch.cuda.current_stream(dev)
     # warm-up: the per-device tables and workspaces (one block row of one slice)
     if ranges:
@@ -530,10 +580,13 @@ def batch_workload(args, gic, world, rank, dev):
 
     def step():
         shard.encode_shard(7, src, n, n, S, 4, rank, world, opts, stream=stream, chunk=chunk, dst=dst)
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
-    wall, kern_ms = _timed(world, dev, stream, step, args.steps)
+    gic.iter_cap_hits(reset=True)
+    wall, kern_ms = _timed(world, dev, stream, step, steps)
     spread = _timed.spread
+    hits = _max_over_ranks(torch.tensor([float(gic.iter_cap_hits(reset=True))], dtype=torch.float64, device=dev),
+                           world)
     gather_ms = None
     full = dst
     if world > 1:
@@ -546,78 +599,88 @@ def batch_workload(args, gic, world, rank, dev):
         g = _max_over_ranks(torch.tensor([gather_ms], dtype=torch.float64, device=dev), world)
         gather_ms = float(g[0])
     total_blocks = S * bx * by
-    line = None
-    if rank == 0:
-        how = ("one contiguous range per rank" if not chunk else
-               f"chunks of {chunk} block rows dealt round-robin")
-        if world == 1:
-            gather = "one rank: no gather"
+    if rank != 0:
+        return None
+    how = "one contiguous range per rank" if not chunk else f"chunks of {chunk} block rows dealt round-robin"
+    if world == 1:
+        gather = "one rank: no gather"
+    else:
+        gather = (f"{'RCCL' if dist.get_backend() != 'gloo' else 'gloo (rehearsal)'} gather to rank 0 "
+                  f"timed separately")
+    if bound > 0:
+        search = (f"bounded exit: blocks whose mode-6/3/1 probe decodes within MSE {bound:g} are final, the rest "
+                  f"{'the exact search (contract met by construction)' if shake_ranks == 0 else 'the pruned search'}")
+    else:
+        search = ("exact (the reference search)" if shake_ranks == 0 else
+                  f"pruned, {shake_ranks} partitions shaken per mode (per-block MSE tolerance)")
+    res = {
+        "metric": f"Mpixels/s BC7 quality {args.bc7_quality:g} on the configs[4] batch, {search}",
+        "value": round(S * n * n * steps / wall / 1e6, 4), "unit": "Mpixels/s", "n_gpus": world, "steps": steps,
+        "warmup": warmup, "ms_per_step": round(wall / steps * 1e3, 3), "scaling": "strong", "dtype": "f64+int32",
+        "config": {"workload": f"configs[4]: BC7 quality {args.bc7_quality:g} on a batch of {S}x{n}x{n} RGBA8 G1 "
+                               f"slices (seed 0x9E3779B9+s), block rows of every slice split over {world} rank(s) "
+                               f"({how}), {gather}",
+                   "format": "BC7", "slices": S, "width": n, "global_batch_blocks": total_blocks,
+                   "bc7_search": search, "parallelism": f"block-row shards x{world}", "shard_chunk_rows": chunk},
+        "blocks_per_s": round(total_blocks * steps / wall, 1),
+        "kernel_ms": round(kern_ms, 3), "kernel_ms_rank_min_max": [round(x, 3) for x in spread],
+        "gather_ms": None if gather_ms is None else round(gather_ms, 3),
+        "iter_cap_hits": int(hits[0]),
+        "roofline": {"bound": "valu", "achieved": round(80 * nblk / (kern_ms * 1e-3) / 1e9, 4),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(80 * nblk / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 8),
+                     "traffic": None, "alg_bytes_per_launch": 80 * nblk,
+                     "note": "VALU bound; HBM fraction (80 B per block) per BASELINE.json"},
+        "cpu_baseline": None,
+    }
+    host = full.cpu().numpy().reshape(S, by, bx, 16) if full is not None and \
+        full.numel() >= total_blocks * 16 else None
+    if not args.no_cpu and host is not None:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        rows, dt, threads = _batch_oracle(args, S, n, bx, by, oracle_cache if oracle_cache is not None else {})
+        same = bad = tot = 0
+        mse_g = mse_c = 0.0
+        for (sl, row), (ref, texels) in rows.items():
+            got = host[sl, row]
+            same += int((got == ref).all(axis=1).sum())
+            tot += bx
+            t = texels.reshape(4, bx, 4, 4).transpose(1, 0, 2, 3).reshape(bx, 16, 4).astype(np.float64)
+            mg = ((oracle_lib.bc7_decode(got).astype(np.float64) - t) ** 2).mean(axis=(1, 2))
+            mc = ((oracle_lib.bc7_decode(ref).astype(np.float64) - t) ** 2).mean(axis=(1, 2))
+            bad += int((mg > mc * 1.001 + 0.5).sum())
+            mse_g += float(mg.sum())
+            mse_c += float(mc.sum())
+        where = ", ".join(f"slice {sl} row {row}" for sl, row in rows)
+        res["cpu_baseline"] = {"value": round(len(rows) * 4 * n / dt / 1e6, 6), "unit": "Mpixels/s",
+                               "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+                               "sample": f"the exact search on {len(rows)} block rows ({where}; {tot} blocks, "
+                                         f"{dt:.1f} s, {threads} threads)",
+                               "blocks_per_s": round(tot / dt, 1)}
+        res["gpu_parity"] = (f"{same}/{tot} blocks of {where}{' (after the gather)' if world > 1 else ''} "
+                             f"bit-identical to the exact oracle, "
+                             f"{bad} outside the per-block MSE contract, mean MSE {mse_g / tot:.4f} vs "
+                             f"{mse_c / tot:.4f}")
+        if shake_ranks == 0 and bound == 0:
+            res["gpu_parity_ok"] = same == tot
         else:
-            gather = (f"{'RCCL' if dist.get_backend() != 'gloo' else 'gloo (rehearsal)'} gather to rank 0 "
-                      f"timed separately")
-        line = {
-            "metric": "Mpixels/s (and blocks/s) BC1 & BC7 on 8K RGBA8 at 1/2/4/8 MI355X",
-            "value": round(S * n * n * args.steps / wall / 1e6, 4),
-            "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(wall / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": None, "dtype": "f64+int32", "data": "synthetic",
-            "config": {"workload": f"configs[4]: BC7 quality {args.bc7_quality:g} on a batch of {S}x{n}x{n} "
-                                   f"RGBA8 G1 slices (seed 0x9E3779B9+s), block rows of every slice split over "
-                                   f"{world} rank(s) ({how}), {gather}",
-                       "format": "BC7", "slices": S, "width": n, "global_batch_blocks": total_blocks,
-                       "bc7_search": ("exact" if args.bc7_shake_ranks == 0 else
-                                      f"pruned, {args.bc7_shake_ranks} partitions shaken per mode "
-                                      f"(per-block MSE tolerance)") +
-                                     (f"; bounded exit: blocks whose mode-6/3/1 probe decodes within MSE "
-                                      f"{args.bc7_mse_bound:g} are final" if args.bc7_mse_bound > 0 else ""),
-                       "parallelism": f"block-row shards x{world}", "shard_chunk_rows": chunk,
-                       "world_size_seen": dist.get_world_size() if world > 1 else 1},
-            "blocks_per_s": round(total_blocks * args.steps / wall, 1),
-            "kernel_ms": round(kern_ms, 3),
-            "kernel_ms_rank_min_max": [round(x, 3) for x in spread],
-            "gather_ms": None if gather_ms is None else round(gather_ms, 3),
-            "roofline": {"bound": "hbm", "achieved": round(80 * nblk / (kern_ms * 1e-3) / 1e9, 4),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(80 * nblk / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 8),
-                         "traffic": None, "alg_bytes_per_launch": 80 * nblk,
-                         "note": "VALU bound; HBM fraction per BASELINE.json"},
-            "cpu_baseline": None,
-        }
-        host_rows = full.cpu().numpy().reshape(S, by, bx, 16) if full is not None and \
-            full.numel() == total_blocks * 16 else None
-        if not args.no_cpu and host_rows is not None:
-            sys.path.insert(0, os.path.join(ROOT, "tests"))
-            import oracle_lib
-            threads = _cpu_threads()
-            sl, row = S - 1, by // 2
-            img = synth.g1(n, n, seed=0x9E3779B9 + sl)
-            c0 = time.perf_counter()
-            ref = oracle_lib.encode_image_bc7(img, quality=args.bc7_quality, first_row=row, num_rows=1,
-                                              threads=threads)
-            dt = time.perf_counter() - c0   # the reference search: the CPU baseline
-            got = host_rows[sl, row]
-            if args.bc7_mse_bound > 0:
-                # bounded exit: the per-block MSE contract against the exact search
-                t = img[4 * row:4 * row + 4, :bx * 4].reshape(4, bx, 4, 4).transpose(1, 0, 2, 3)
-                t = t.reshape(bx, 16, 4).astype(np.float64)
-                mg = ((oracle_lib.bc7_decode(got).astype(np.float64) - t) ** 2).mean(axis=(1, 2))
-                mc = ((oracle_lib.bc7_decode(ref).astype(np.float64) - t) ** 2).mean(axis=(1, 2))
-                contract = (f"; {int((mg > mc * 1.001 + 0.5).sum())} blocks outside the MSE contract vs the "
-                            f"exact search, mean MSE {mg.mean():.4f} vs {mc.mean():.4f}, "
-                            f"{int((mg <= args.bc7_mse_bound).sum())}/{bx} within the exit bound")
-            else:
-                contract = ""
-            if args.bc7_shake_ranks:
-                ref = oracle_lib.encode_image_bc7(img, quality=args.bc7_quality, first_row=row, num_rows=1,
-                                                  threads=threads, shake_ranks=args.bc7_shake_ranks)
-            same = int((got == ref).all(axis=1).sum())
-            line["cpu_baseline"] = {"value": round(4 * n / dt / 1e6, 6), "unit": "Mpixels/s", "cores": threads,
-                                    "kind": "port", "cpu_model": cpu_model(),
-                                    "sample": f"slice {sl} block row {row} ({bx} blocks, {dt:.1f} s)",
-                                    "blocks_per_s": round(bx / dt, 1)}
-            line["gpu_parity"] = (f"{same}/{bx} blocks of slice {sl} row {row} (after the gather) bit-identical "
-                                  f"to the oracle running the same search" +
-                                  (" without the exit" if args.bc7_mse_bound > 0 else "") + contract)
+            res["gpu_parity_ok"] = bad == 0
+    return res
+
+
+def batch_workload(args, gic, world, rank, dev):
+    """--workload batch64: configs[4] as the headline line (batch_run)."""
+    import torch.distributed as dist
+    res = batch_run(args, gic, world, rank, dev, args.bc7_mse_bound, args.bc7_shake_ranks, args.steps, args.warmup)
+    if rank == 0:
+        line = {"metric": "Mpixels/s (and blocks/s) BC1 & BC7 on 8K RGBA8 at 1/2/4/8 MI355X",
+                "value": res["value"], "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": res["ms_per_step"], "higher_is_better": True,
+                "scaling": "strong", "vs_baseline": None, "dtype": "f64+int32", "data": "synthetic",
+                "config": dict(res["config"], world_size_seen=dist.get_world_size() if world > 1 else 1)}
+        for k in ("blocks_per_s", "kernel_ms", "kernel_ms_rank_min_max", "gather_ms", "iter_cap_hits", "roofline",
+                  "cpu_baseline", "gpu_parity"):
+            line[k] = res.get(k)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
@@ -725,6 +788,22 @@ def main():
             bc45[f"bc{f}"] = bc45_leg(args, gic, f, world, dev, rank)
     if fmt == 1 and args.bc6h_size > 0:
         bc45["bc6h"] = bc6h_leg(args, gic, world, dev, rank)
+        bc45["bc6h_signed"] = bc6h_leg(args, gic, world, dev, rank, signed=True)
+    batch = {}
+    if fmt == 1 and not args.no_batch:
+        # configs[4] at its size: the 64 x 4096^2 G1 stack, one pass each of the
+        # bounded exit (exact survivors) and the exact reference search, block
+        # rows dealt over the ranks, one gather to rank 0, oracle rows checked
+        from gfx_imagecompress_amd import synth
+        bsrc = synth.g1_torch(args.batch_size, args.batch_size, args.batch_slices, seed=0x9E3779B9, device=dev)
+        cache = {}
+        batch["batch64_bounded"] = batch_run(args, gic, world, rank, dev, args.bc7_mse_bound or 0.5, 0, 1, 0,
+                                             src=bsrc, oracle_cache=cache)
+        if not args.no_batch_exact:
+            batch["batch64_exact"] = batch_run(args, gic, world, rank, dev, 0.0, 0, 1, 0, src=bsrc,
+                                               oracle_cache=cache)
+        del bsrc
+        torch.cuda.empty_cache()
 
     cpu = None
     parity = None
@@ -776,6 +855,7 @@ def main():
         line.update(bounded)
         line.update(enc16)
         line.update(bc45)
+        line.update(batch)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

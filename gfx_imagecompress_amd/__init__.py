@@ -164,6 +164,10 @@ def library() -> ctypes.CDLL:
     lib.gic_block_bytes.restype = u32
     lib.gic_last_hip_error.restype = ctypes.c_int
     lib.gic_version.restype = ctypes.c_char_p
+    lib.gic_iter_cap_hits.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    lib.gic_iter_cap_hits.restype = ctypes.c_int
+    lib.gic_set_iter_cap.argtypes = [ctypes.c_int]
+    lib.gic_set_iter_cap.restype = ctypes.c_int
     _lib = lib
     return lib
 
@@ -174,6 +178,21 @@ def _check(rc: int) -> None:
         if rc == GIC_EHIP:
             extra = f" (hipError {library().gic_last_hip_error()})"
         raise GicError(f"gic call failed: {_ERRS.get(rc, rc)}{extra}")
+
+
+def iter_cap_hits(reset: bool = False) -> int:
+    """Quantiser loops the GPU stopped at the iteration cap on the current
+    device (gic_iter_cap_hits): blocks where the reference would
+    not have returned."""
+    n = ctypes.c_ulonglong(0)
+    _check(library().gic_iter_cap_hits(ctypes.byref(n), 1 if reset else 0))
+    return int(n.value)
+
+
+def set_iter_cap(cap: int) -> None:
+    """The iteration cap (rounds past the never-reset counter's exhaustion;
+    < 0 restores the default 4096).  A test hook."""
+    _check(library().gic_set_iter_cap(int(cap)))
 
 
 def block_bytes(fmt: int) -> int:

@@ -48,6 +48,8 @@ hipError_t launch_bc7enc_blocks_f32(const float *blocks, uint32_t n, const gic_o
 hipError_t launch_bc6h_blocks(const float *blocks, uint32_t n, int is_signed, void *dst, double *err, hipStream_t s);
 hipError_t launch_bc6h_image(const Geometry &g, int is_signed, int force_alpha_one, void *dst, double *err,
                              hipStream_t s);
+hipError_t bc7_iter_cap(int cap, unsigned long long *hits, int reset);
+hipError_t bc6h_iter_cap(int cap, unsigned long long *hits, int reset);
 }  // namespace gic
 
 static bool is_bc6h(gic_format f) { return f == GIC_FMT_BC6H || f == GIC_FMT_BC6H_SF; }
@@ -64,6 +66,27 @@ static int hip_fail(hipError_t e)
 }
 
 extern "C" int gic_last_hip_error(void) { return t_last_hip_error; }
+
+extern "C" int gic_iter_cap_hits(unsigned long long *hits, int reset)
+{
+    if (!hits) return GIC_EINVAL;
+    unsigned long long a = 0, b = 0;
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = gic::bc7_iter_cap(-1, &a, reset);
+    if (e == hipSuccess) e = gic::bc6h_iter_cap(-1, &b, reset);
+    if (e != hipSuccess) return hip_fail(e);
+    *hits = a + b;
+    return GIC_OK;
+}
+
+extern "C" int gic_set_iter_cap(int cap)
+{
+    if (cap < 0) cap = 4096;
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = gic::bc7_iter_cap(cap, nullptr, 0);
+    if (e == hipSuccess) e = gic::bc6h_iter_cap(cap, nullptr, 0);
+    return e == hipSuccess ? GIC_OK : hip_fail(e);
+}
 
 extern "C" const char *gic_version(void) { return "gfx_imagecompress_amd 0.1 (gfx950)"; }
 

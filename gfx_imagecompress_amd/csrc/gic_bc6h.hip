@@ -255,6 +255,13 @@ __device__ __forceinline__ uint64_t pack_idx(const int idx[16], uint32_t mask)
     return v;
 }
 
+// Iteration cap, as gic_bc7.hip: optQuantAnD_f's requantisation
+// loop never resets try_two (amd_hdr_encode.cpp:1427-1601), so past its
+// exhaustion the reference loops until the state is stable; the GPU stops
+// g_iter_cap rounds later and counts the hit (gic_iter_cap_hits).
+__device__ int g_iter_cap = 4096;
+__device__ unsigned long long g_iter_hits = 0;
+
 // optQuantAnD_f (amd_hdr_encode.cpp:1427-1601), dimension 3, quality 1.0, over
 // the members of `mask` (data = din, texel-indexed).  Returns the error; idx
 // (texel-indexed) and the GetEndPoints (:1116-1159) end points ep[2][3].
@@ -331,7 +338,6 @@ __device__ __forceinline__ float opt_quant_f(const float din[16][3], uint32_t ma
         }
         if (it) {
             bool done;
-            int inner = 0;
             do {
                 float q = 0, s = 0, t = 0;
 #pragma unroll
@@ -371,7 +377,10 @@ __device__ __forceinline__ float opt_quant_f(const float din[16][3], uint32_t ma
                         done = done && cnt == idx[k];
                         idx[k] = cnt;
                     }
-                if (++inner > 4096) break;   // the reference loops until done once try_two < 0 (orc_bc6h.c)
+                if (try_two < -g_iter_cap) {   // H4: the reference loops until done once try_two < 0
+                    atomicAdd(&g_iter_hits, 1ull);
+                    break;
+                }
             } while (!done && try_two--);
             if (it == 1) {
                 snap = pack_idx(idx, mask);
@@ -1417,6 +1426,18 @@ static hipError_t bc6h_run(const float *blocks, const Geometry *g, uint32_t n, i
     }
     const hipError_t ef = hipFreeAsync(mem, s);
     return e != hipSuccess ? e : ef;
+}
+
+hipError_t bc6h_iter_cap(int cap, unsigned long long *hits, int reset)
+{
+    hipError_t e = hipSuccess;
+    if (hits) e = hipMemcpyFromSymbol(hits, HIP_SYMBOL(bc6h::g_iter_hits), sizeof(*hits));
+    if (e == hipSuccess && reset) {
+        const unsigned long long z = 0;
+        e = hipMemcpyToSymbol(HIP_SYMBOL(bc6h::g_iter_hits), &z, sizeof(z));
+    }
+    if (e == hipSuccess && cap >= 0) e = hipMemcpyToSymbol(HIP_SYMBOL(bc6h::g_iter_cap), &cap, sizeof(cap));
+    return e;
 }
 
 hipError_t launch_bc6h_blocks(const float *blocks, uint32_t n, int is_signed, void *dst, double *err, hipStream_t s)

@@ -145,6 +145,22 @@ __device__ __forceinline__ int anchor_of(int subsets, int part, int s)
     return s == 1 ? dAnchor3a[part] : dAnchor3b[part];
 }
 
+// Iteration cap: optQuantAnD_d's requantisation loop
+// `do ... while (!done && try_two--)` (amd_bc7_3dquant_vpc.cpp:1885,1986) never
+// resets try_two, so once it has run negative the reference loops until the
+// requantisation is stable -- forever on a cycling state.  The GPU stops such a
+// loop g_iter_cap rounds past the counter's exhaustion and counts the hit
+// (gic_iter_cap_hits); no tested input reaches it.
+__device__ int g_iter_cap = 4096;
+__device__ unsigned long long g_iter_hits = 0;
+
+__device__ __forceinline__ bool iter_capped(int try_two, int cap)
+{
+    if (try_two >= -cap) return false;
+    atomicAdd(&g_iter_hits, 1ull);
+    return true;
+}
+
 __device__ __forceinline__ int clog_of(int last)
 {
     int c = 0, i = last + 1;
@@ -354,9 +370,9 @@ __device__ double opt_quant(const double data[][4], int n, int ncl, int *index, 
                     index[j] = nidx[j];
                 }
                 // the reference's counter is never reset; past zero the loop
-                // runs until the requantisation is stable.  A cap keeps the GPU
-                // bounded; it is far above anything observed.
-                if (try_two < -4096) break;
+                // runs until the requantisation is stable.  The cap keeps the
+                // GPU bounded and counts the hit (g_iter_hits).
+                if (iter_capped(try_two, g_iter_cap)) break;
             } while (!done && try_two--);
             if (it == 1) {
                 for (int j = 0; j < n; ++j) snap[j] = index[j];
@@ -391,6 +407,8 @@ __device__ double opt_quant(const double data[][4], int n, int ncl, int *index, 
     return err;
 }
 
+#define GIC_QUANT_CAP g_iter_cap
+#define GIC_QUANT_CAP_HIT atomicAdd(&g_iter_hits, 1ull)
 #include "bc7_quant.inc"
 
 // ------------------------------------ exhaustive quantiser (performance < 1) ---
@@ -3019,6 +3037,20 @@ hipError_t launch_bc7_blocks(const float *blocks, uint32_t n, const gic_options 
     return bc7::run_chunks(nullptr, blocks, n, o, dst, err, s);
 }
 
+}  // namespace gic
+
+namespace gic {
+hipError_t bc7_iter_cap(int cap, unsigned long long *hits, int reset)
+{
+    hipError_t e = hipSuccess;
+    if (hits) e = hipMemcpyFromSymbol(hits, HIP_SYMBOL(bc7::g_iter_hits), sizeof(*hits));
+    if (e == hipSuccess && reset) {
+        const unsigned long long z = 0;
+        e = hipMemcpyToSymbol(HIP_SYMBOL(bc7::g_iter_hits), &z, sizeof(z));
+    }
+    if (e == hipSuccess && cap >= 0) e = hipMemcpyToSymbol(HIP_SYMBOL(bc7::g_iter_cap), &cap, sizeof(cap));
+    return e;
+}
 }  // namespace gic
 
 #ifdef GIC_PROFILE

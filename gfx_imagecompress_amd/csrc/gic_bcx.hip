@@ -1212,15 +1212,41 @@ __device__ uint64_t encode_bc4(const float v[16])
 {
     // ascending sort by rank (equal values are interchangeable)
     float s[16];
+    bool nan = false;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        int r = 0;
+    for (int i = 0; i < 16; ++i) nan = nan || v[i] != v[i];
+    if (!nan) {
 #pragma unroll
-        for (int j = 0; j < 16; ++j) r += (v[j] < v[i] || (v[j] == v[i] && j < i)) ? 1 : 0;
-        // scatter through a select chain keeps s[] in registers
+        for (int i = 0; i < 16; ++i) {
+            int r = 0;
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
-            if (r == k) s[k] = v[i];
+            for (int j = 0; j < 16; ++j) r += (v[j] < v[i] || (v[j] == v[i] && j < i)) ? 1 : 0;
+            // scatter through a select chain keeps s[] in registers
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (r == k) s[k] = v[i];
+        }
+    } else {
+        // A NaN texel (float sources only): QSortFCmp (:1609-1618) calls a NaN
+        // equal to everything, which is no total order, so the reference's
+        // qsort result is undefined (C11 7.22.5p4) and ranks would leave holes.
+        // The order is the oracle's insertion sort's (orc_bcx.c
+        // scalar_endpoints): each value moves left past larger ones only, as
+        // a static chain of selects.
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[i] = v[i];
+#pragma unroll
+        for (int i = 1; i < 16; ++i) {
+            const float t = s[i];
+            bool go = true;
+#pragma unroll
+            for (int j = i - 1; j >= 0; --j) {
+                const bool mv = go && (s[j] - t) > 0.0f;
+                s[j + 1] = mv ? s[j] : (go ? t : s[j + 1]);
+                go = mv;
+            }
+            s[0] = go ? t : s[0];
+        }
     }
     uint8_t ep8[2], ep6[2];
     uint64_t i8, i6 = 0;

@@ -15,15 +15,18 @@ namespace gic {
 
 // RN(d / 3): q0 = d * RN(1/3), r = d - 3 q0 exactly (FMA), q = q0 + r * RN(1/3);
 // the sign of an exact zero follows d.  Equal to d / 3.0f for every finite d
-// (the check's only mismatches are d = +-inf, which the BC1 search never
-// divides: its dividends are differences and sums of bounded projections and
-// colour values)
+// (tools/rcp_check.hip over all 2^32 inputs); a non-finite d is returned as it
+// is -- inf / 3 = inf, and a NaN keeps its payload as the division would --
+// where the sequence above would give NaN for +-inf.  The BC1 search divides
+// such values only on unbounded float block inputs (huge or infinite texels
+// through Image_CompressAMDBC1Block / GIC_SRC_FLOAT32).
 GIC_FD float div3_rn(float d)
 {
     const float C = 0x1.555556p-2f;
     const float q0 = d * C;
     const float r = __builtin_fmaf(-q0, 3.0f, d);
-    return __builtin_copysignf(__builtin_fmaf(r, C, q0), d);
+    const float q = __builtin_copysignf(__builtin_fmaf(r, C, q0), d);
+    return __builtin_isfinite(d) ? q : d;
 }
 
 #ifndef GIC_FASTDIV_HOST

@@ -179,6 +179,19 @@ int gic_last_hip_error(void);
  * a failed one writes a zero block, prints to stderr and sets this status. */
 int gic_block_last_status(void);
 
+/* Iteration caps.  The reference's BC7 and BC6H quantisers
+ * (optQuantAnD_d, amd_bc7_3dquant_vpc.cpp:1885-1986; optQuantAnD_f,
+ * amd_hdr_encode.cpp:1427-1601) requantise in `do ... while (!done && try_two--)`
+ * with a counter that is never reset: once it has run negative the loop runs
+ * until the requantisation is stable, forever on a cycling state.  The GPU
+ * stops such a loop `cap` rounds past the counter's exhaustion (default 4096)
+ * and counts each stop on the current device; a block with a hit differs from
+ * the reference, which would not have returned.
+ *   gic_iter_cap_hits: the count since the last reset (synchronises the device);
+ *   gic_set_iter_cap: the cap (< 0 restores 4096; a small cap is a test hook). */
+int gic_iter_cap_hits(unsigned long long *hits, int reset);
+int gic_set_iter_cap(int cap);
+
 /* Library version string. */
 const char *gic_version(void);
 

@@ -1,6 +1,6 @@
 // Host check of gic::div3_rn (csrc/gic_fastdiv.h) against IEEE float division:
-// every STRIDE-th float bit pattern (argv[1]), infinities and NaNs skipped (the
-// BC1 search never divides them).  The GPU check over all 2^32 inputs, including
+// every STRIDE-th float bit pattern (argv[1]) plus +-inf and NaNs: equal bit
+// patterns, or both NaN (a NaN keeps its payload as the division would).  The GPU check over all 2^32 inputs, including
 // rcp_rn, is tools/rcp_check.hip.
 #define GIC_FASTDIV_HOST
 #include <cmath>
@@ -14,14 +14,14 @@ int main(int argc, char **argv)
 {
     const uint64_t stride = argc > 1 ? strtoull(argv[1], nullptr, 10) : 7;
     uint64_t n = 0, bad = 0;
-    for (uint64_t u = 0; u < (1ull << 32); u += stride) {
-        const uint32_t b = (uint32_t)u;
+    const uint32_t extra[] = {0x7f800000u, 0xff800000u, 0x7fc00000u, 0xffc00000u, 0x7fc12345u, 0x7f7fffffu, 0xff7fffffu};
+    for (uint64_t u = 0; u < (1ull << 32) + sizeof(extra) / 4 * stride; u += stride) {
+        const uint32_t b = u < (1ull << 32) ? (uint32_t)u : extra[(u - (1ull << 32)) / stride];
         float d;
         memcpy(&d, &b, 4);
-        if (!std::isfinite(d)) continue;
         ++n;
         const float q = gic::div3_rn(d), r = d / 3.0f;
-        if (memcmp(&q, &r, 4) != 0) ++bad;
+        if (memcmp(&q, &r, 4) != 0 && !(std::isnan(q) && std::isnan(r))) ++bad;
     }
     printf("%llu/%llu mismatches\n", (unsigned long long)bad, (unsigned long long)n);
     return bad ? 1 : 0;

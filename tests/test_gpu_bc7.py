@@ -281,3 +281,37 @@ def test_bc7_dual_index_regression_blocks(gpu, mask):
         for i, b in enumerate(blocks):
             enc, _ = oracle_lib.bc7_block(b, mask)
             assert got[i].tobytes() == enc, (mask, i)
+
+
+def test_iteration_cap_hits_are_counted(gpu):
+    """the reference's requantisation loop (optQuantAnD_d,
+    amd_bc7_3dquant_vpc.cpp:1885-1986; optQuantAnD_f for BC6H) never resets its
+    counter, so past its exhaustion it runs until the state is stable.  The GPU
+    stops such a loop at a cap and counts the stop (gic_iter_cap_hits).  At the
+    default cap a G1 band and an HDR image reach it nowhere (the output equals
+    the oracle's); with the cap at 0 (every loop stopped as soon as the
+    reference's counter runs out -- blocks that need more requantisation
+    passes than its budget of 50) the counter reports the stops."""
+    import torch
+    img = synth.g1(256, 64)
+    hdr = synth.hdr_rgba(256, 256, seed=3)
+    src = torch.from_numpy(hdr.reshape(-1).copy()).cuda()
+    dst = torch.zeros(64 * 64 * 16, dtype=torch.uint8, device="cuda")
+    gic.iter_cap_hits(reset=True)
+    out = gpu_encode(7, img)
+    assert gic.iter_cap_hits(reset=True) == 0
+    assert np.array_equal(out[:64], oracle_lib.encode_image_bc7(img, first_row=0, num_rows=1))
+    gic.encode_device_src(gic.FMT_BC6H, gic.SRC_FLOAT32, src, 256, 256, 1, 4, dst)
+    assert gic.iter_cap_hits(reset=True) == 0
+    gic.set_iter_cap(0)
+    try:
+        gpu_encode(7, img)
+        hits7 = gic.iter_cap_hits(reset=True)
+        gic.encode_device_src(gic.FMT_BC6H, gic.SRC_FLOAT32, src, 256, 256, 1, 4, dst)
+        hits6 = gic.iter_cap_hits(reset=True)
+    finally:
+        gic.set_iter_cap(-1)
+    print(f"\ncap 0: {hits7} BC7 and {hits6} BC6H quantiser loops stopped")
+    assert hits7 > 0 and hits6 > 0
+    gpu_encode(7, img[:8])
+    assert gic.iter_cap_hits(reset=True) == 0   # the default cap is back

@@ -110,7 +110,9 @@ def _fixture(name, n):
 @pytest.mark.parametrize("name,meta", _cases() or [pytest.param("missing", {}, marks=pytest.mark.skip)])
 def test_bc7_sample_8d(gpu, name, meta, shake_ranks):
     rows = meta["rows"]
+    gic.iter_cap_hits(reset=True)
     got = _encode_rows(name, rows, shake_ranks)
+    assert gic.iter_cap_hits(reset=True) == 0   # H4: no quantiser loop reached the GPU's iteration cap
     ref = _fixture(name, got.shape[0])
     src = _src_of(name, rows)
     mg, mc = _block_mse(got, src), _block_mse(ref, src)

@@ -386,3 +386,45 @@ def test_host_api_snorm_source_gives_snorm_destination(gpu):
     assert out.tobytes() == dst.cpu().numpy().tobytes()
     lib.Image_Destroy(q)
     lib.Image_Destroy(p)
+
+
+def _special_blocks(kind, n=48, seed=0):
+    """Float blocks in [0, 1) with some texels replaced by values the reference
+    reads unclamped (block_utils.cpp:7-41): huge finite (their x255 scale or
+    the search's hi - lo differences overflow to inf), +-inf, or NaN."""
+    rng = np.random.default_rng(seed)
+    b = rng.random((n, 16, 4), dtype=np.float32)
+    b[::2, :, 3] = 1.0
+    vals = {"huge": [1e36, 3.0e38, -3.0e38, 2.0e37], "inf": [np.inf, -np.inf], "nan": [np.nan]}[kind]
+    for i in range(n):
+        for _ in range(1 + i % 3):
+            t, c = int(rng.integers(16)), int(rng.integers(4 if i % 4 == 3 else 3))
+            b[i, t, c] = np.float32(vals[int(rng.integers(len(vals)))])
+    return b
+
+
+@pytest.mark.parametrize("kind", ["huge", "inf", "nan"])
+def test_bc1_bc3_non_finite_float_texels(gpu, kind):
+    """Huge, infinite and NaN float texels through the BC1 block API
+    (Image_CompressAMDBC1Block), and through the FLOAT32 source path for BC1
+    and BC3, against the oracle (the search's fast division by 3 returns +-inf
+    and NaN as IEEE division does, gic_fastdiv.h)."""
+    import torch
+    lib = gic.library()
+    blocks = _special_blocks(kind)
+    for i, blk in enumerate(blocks):
+        out = np.zeros(8, np.uint8)
+        lib.Image_CompressAMDBC1Block(np.ascontiguousarray(blk).ctypes.data_as(ctypes.c_void_p), False, False, 1,
+                                      ctypes.c_float(128 / 255.0), out.ctypes.data_as(ctypes.c_void_p))
+        assert out.tobytes() == oracle_lib.bc1_block(blk), (kind, i)
+    # the same blocks as a 4 x 12-block FLOAT32 image
+    tex = blocks.reshape(4, 12, 4, 4, 4).transpose(0, 2, 1, 3, 4).reshape(16, 48, 4)
+    src = torch.from_numpy(np.ascontiguousarray(tex)).cuda()
+    for fmt in (1, 3):
+        dst = torch.zeros(48 * gic.block_bytes(fmt), dtype=torch.uint8, device="cuda")
+        gic.encode_device_src(fmt, gic.SRC_FLOAT32, src, 48, 16, 1, 4, dst)
+        torch.cuda.synchronize()
+        got = dst.cpu().numpy().reshape(-1, gic.block_bytes(fmt))
+        for i, b in enumerate(_float_blocks(tex, 48, 16)):
+            ref = oracle_lib.bc1_block(b) if fmt == 1 else oracle_lib.bc23_block(3, b)
+            assert got[i].tobytes() == ref, (kind, fmt, i)
