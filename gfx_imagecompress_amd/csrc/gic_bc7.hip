@@ -116,7 +116,14 @@ struct Workspace {
     uint8_t *prank;        // [n][6][8] partition of stable rank r of each single-index slot (k_rank)
     uint64_t *pqidx;       // [n][6][8] its optQuantAnD_d indices (k_rank), so a shake wave's loads are independent
     uint32_t *px;          // [n][16] texels packed R | G << 8 | B << 16 | A << 24 (integral blocks; k_prep)
+    uint32_t *defer;       // [n][kDeferPer] shake problems the fast wave kernels handed to the slow ones
+    uint32_t *defer_cnt;   // [4] their counts per kernel kind (zeroed per run_modes)
 };
+
+// Deferred shake problems (bc7_wave.inc FAST): list regions per kernel kind --
+// k_shake_wave<8> (40 problems per block), <4> (56), <16> (1), k_dual_wave (24)
+constexpr int kDeferPer = 121;
+__host__ __device__ constexpr uint32_t defer_off(int kind) { return kind == 0 ? 0u : (kind == 1 ? 40u : (kind == 2 ? 96u : 97u)); }
 
 __device__ __forceinline__ int expand_code(int bits, int v) { return (v << (8 - bits)) | (v >> (2 * bits - 8)); }
 
@@ -1868,15 +1875,15 @@ __global__ void __launch_bounds__(256) k_rank(Params p, Workspace ws)
 }
 
 // K2 (waves): one wavefront per (block, mode, rank, subset) shake problem of
-// an integral block
-template <int NC>
-__global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, const SpEntry *__restrict__ sp)
+// an integral block.  Returns false when the FAST form deferred the problem
+// (bc7_wave.inc: it reached quant_single_point_d); nothing is written then.
+template <int NC, bool FAST>
+__device__ __forceinline__ bool shake_problem(const Params &p, const Workspace &ws, const SpEntry *__restrict__ sp,
+                                              uint32_t wid)
 {
-    // wave-uniform by construction; readfirstlane lets the compiler see it (scalar loads and branches)
-    const uint32_t wid = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t per = (uint32_t)wave_count<NC>(p.att);
     const uint32_t b = wid / per;
-    if (b >= p.n) return;
+    if (b >= p.n) return true;
     int slot, rank, subset;
     wave_problem<NC>(p, (int)(wid % per), slot, rank, subset);
     const int mode = kSlotMode[slot];
@@ -1895,9 +1902,9 @@ __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, c
     const uint64_t qidx = nparts == 1 ? ws.qidx[(size_t)b * kQuantTasks + kSlotBase[slot]] : ws.pqidx[sr + rank];
     const int lpart = ln < rank ? (int)ws.prank[sr + ln] : 0;   // lane L < rank: the partition of rank L
     const uint32_t pxl = ln < 16 ? ws.px[(size_t)b * 16 + ln] : 0u;
-    if (!mode_active(meta, p, mode) || (meta.flags & 3u) != 2u) return;
+    if (!mode_active(meta, p, mode) || (meta.flags & 3u) != 2u) return true;
     const ModeInfo &mi = kModes[mode];
-    if (rank >= mode_attempts(p, mode)) return;
+    if (rank >= mode_attempts(p, mode)) return true;
     const ShakeCfg cfg = shake_cfg(mode, p.quality);
     // gather the subset: lane L < n holds the L-th texel of the subset
     uint32_t mask = 0;
@@ -1929,7 +1936,7 @@ __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, c
                 if (subset == 0) res.part = (uint32_t)part;
                 res.err[subset] = -1.0 - (double)key;
             }
-            return;
+            return true;
         }
     }
     const int n = __popc(mask);
@@ -1950,8 +1957,11 @@ __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, c
     PROF_BEGIN;
     int epo[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
     const bool corners_too = !(meta.max_range > p.shake_thr) && cfg.dim == 3;
-    const double e = wv::subset_shake<NC>(sp, T, idx, epo, corners_too, cfg.shake, cfg.last, cfg.bits, cfg.parity);
+    bool defer = false;
+    const double e = wv::subset_shake<NC, FAST>(sp, T, idx, epo, corners_too, cfg.shake, cfg.last, cfg.bits, cfg.parity,
+                                                defer);
     PROF_END;
+    if (FAST && defer) return false;
     unsigned long long ti = T.live ? (unsigned long long)(idx & 15) << (4 * src) : 0ull;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) ti |= __shfl_xor(ti, o);
@@ -1964,7 +1974,46 @@ __global__ void __launch_bounds__(256, 4) k_shake_wave(Params p, Workspace ws, c
             res.ep[subset][1][k] = (uint8_t)epo[1][k];
         }
     }
+    return true;
 }
+
+// Fast form: the problems that reach quant_single_point_d are appended to
+// the kind's deferred list (one atomic per such wave) for k_shake_wave_slow.
+__device__ __forceinline__ void defer_push(const Params &p, const Workspace &ws, int kind, uint32_t wid)
+{
+    if (wv::lane() == 0) {
+        const uint32_t k = atomicAdd(&ws.defer_cnt[kind], 1u);
+        ws.defer[(size_t)defer_off(kind) * p.n + k] = wid;
+    }
+}
+
+// waves per SIMD of the fast kernels (<= 72 / 64 / 80 VGPRs, no spills)
+template <int NC> struct ShakeOcc { static constexpr int v = 7; };
+template <> struct ShakeOcc<4> { static constexpr int v = 8; };
+template <> struct ShakeOcc<16> { static constexpr int v = 6; };   // 16 ramp points per corner lane
+template <int NC> constexpr int shake_kind() { return NC == 8 ? 0 : (NC == 4 ? 1 : 2); }
+
+template <int NC>
+__global__ void __launch_bounds__(256, ShakeOcc<NC>::v) k_shake_wave(Params p, Workspace ws, const SpEntry *__restrict__ sp)
+{
+    // wave-uniform by construction; readfirstlane lets the compiler see it (scalar loads and branches)
+    const uint32_t wid = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    if (!shake_problem<NC, true>(p, ws, sp, wid)) defer_push(p, ws, shake_kind<NC>(), wid);
+}
+
+// The deferred problems, whole, with the quant_single_point_d branch: a grid of
+// a few waves per SIMD strides over the list the fast kernel left (read after
+// it completed, same stream).
+template <int NC>
+__global__ void __launch_bounds__(256, 4) k_shake_wave_slow(Params p, Workspace ws, const SpEntry *__restrict__ sp)
+{
+    const uint32_t w0 = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(ws.defer_cnt[shake_kind<NC>()]);
+    const uint32_t *list = ws.defer + (size_t)defer_off(shake_kind<NC>()) * p.n;
+    for (uint32_t i = w0; i < cnt; i += nw) shake_problem<NC, false>(p, ws, sp, __builtin_amdgcn_readfirstlane(list[i]));
+}
+
 
 // K3a: dual-index quantisation (CompressDualIndexBlock :1084-1152): optQuantAnD_d
 // for the colour and the replicated-alpha halves of each (rotation, selection);
@@ -2114,12 +2163,12 @@ __global__ void __launch_bounds__(64) k_dual_quant_trace(Params p, Workspace ws)
 
 // K3b (waves): shakers of one half of a dual-index candidate
 // (CompressDualIndexBlock :1158-1254); integral blocks
-__global__ void __launch_bounds__(256, 4) k_dual_wave(Params p, Workspace ws, const SpEntry *__restrict__ sp)
+template <bool FAST>
+__device__ __forceinline__ bool dual_problem(const Params &p, const Workspace &ws, const SpEntry *__restrict__ sp,
+                                             uint32_t wid)
 {
-    // wave-uniform by construction; readfirstlane lets the compiler see it (scalar loads and branches)
-    const uint32_t wid = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t b = wid / (kDualTasks * 2), r = wid % (kDualTasks * 2);
-    if (b >= p.n) return;
+    if (b >= p.n) return true;
     const uint32_t task = r >> 1, half = r & 1;
     const int mode = task < 8 ? 4 : 5;
     const int rot = task < 8 ? (int)(task >> 1) : (int)(task - 8);
@@ -2129,10 +2178,10 @@ __global__ void __launch_bounds__(256, 4) k_dual_wave(Params p, Workspace ws, co
     const BlockMeta meta = ws.meta[b];
     const uint32_t pxl = ln < 16 ? ws.px[(size_t)b * 16 + ln] : 0u;   // lane t < 16: texel t, packed
     const uint64_t qi = ws.dqidx[((size_t)b * kDualTasks + task) * 2 + half];
-    if (!mode_active(meta, p, mode) || (meta.flags & 3u) != 2u) return;
+    if (!mode_active(meta, p, mode) || (meta.flags & 3u) != 2u) return true;
     if (!dual_shaken(p, ws, b, (int)task)) {   // not shaken: never selected
         if (ln == 0) ws.dual[(size_t)b * kDualTasks + task].err[half] = 1.7976931348623157e308;
-        return;
+        return true;
     }
     const int shake = dual_shake_size(p);
     const ModeInfo &mi = kModes[mode];
@@ -2151,13 +2200,17 @@ __global__ void __launch_bounds__(256, 4) k_dual_wave(Params p, Workspace ws, co
     wv::Round0 none;
     none.valid = false;
     double e;
+    bool defer = false;
     if (last == 3) {
-        if (corners_too) wv::corners<4>(sp, T, idx, epo, last, bits, PAR_CART, none);   // Q9: error ignored
-        e = wv::window<4, 3>(sp, T, idx, epo, shake, last, bits[3], none);
+        if (corners_too) wv::corners<4, FAST>(sp, T, idx, epo, last, bits, PAR_CART, none, defer);   // Q9: error ignored
+        if (FAST && defer) return false;
+        e = wv::window<4, 3, FAST>(sp, T, idx, epo, shake, last, bits[3], none, defer);
     } else {
-        if (corners_too) wv::corners<8>(sp, T, idx, epo, last, bits, PAR_CART, none);
-        e = wv::window<8, 3>(sp, T, idx, epo, shake, last, bits[3], none);
+        if (corners_too) wv::corners<8, FAST>(sp, T, idx, epo, last, bits, PAR_CART, none, defer);
+        if (FAST && defer) return false;
+        e = wv::window<8, 3, FAST>(sp, T, idx, epo, shake, last, bits[3], none, defer);
     }
+    if (FAST && defer) return false;
     unsigned long long ti = T.live ? (unsigned long long)(idx & 15) << (4 * ln) : 0ull;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) ti |= __shfl_xor(ti, o);
@@ -2170,6 +2223,23 @@ __global__ void __launch_bounds__(256, 4) k_dual_wave(Params p, Workspace ws, co
             res.ep[half][1][k] = (uint8_t)epo[1][k];
         }
     }
+    return true;
+}
+
+__global__ void __launch_bounds__(256, 8) k_dual_wave(Params p, Workspace ws, const SpEntry *__restrict__ sp)
+{
+    // wave-uniform by construction; readfirstlane lets the compiler see it (scalar loads and branches)
+    const uint32_t wid = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    if (!dual_problem<true>(p, ws, sp, wid)) defer_push(p, ws, 3, wid);
+}
+
+__global__ void __launch_bounds__(256, 4) k_dual_wave_slow(Params p, Workspace ws, const SpEntry *__restrict__ sp)
+{
+    const uint32_t w0 = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(ws.defer_cnt[3]);
+    const uint32_t *list = ws.defer + (size_t)defer_off(3) * p.n;
+    for (uint32_t i = w0; i < cnt; i += nw) dual_problem<false>(p, ws, sp, __builtin_amdgcn_readfirstlane(list[i]));
 }
 
 // K3 (f64 lanes): dual-index candidates of blocks with fractional texels
@@ -2705,7 +2775,8 @@ static hipError_t get_state(uint32_t chunk, int nsets, DeviceState *&out)
                           align_up(n * kDualTasks * 2 * sizeof(double)) + align_up(n * sizeof(double)) +
                           align_up(n * sizeof(uint4)) + align_up(n * kUMax * sizeof(double)) +
                           align_up(n * kUMax * sizeof(uint64_t)) +
-                          align_up(n * kShakeSlots * kShakeRanks * sizeof(uint64_t)) + align_up(n * 16 * sizeof(uint32_t));
+                          align_up(n * kShakeSlots * kShakeRanks * sizeof(uint64_t)) + align_up(n * 16 * sizeof(uint32_t)) +
+                          align_up(n * kDeferPer * sizeof(uint32_t)) + align_up(4 * sizeof(uint32_t));
         e = hipMalloc(&st.ws_mem[k], sz);
         if (e != hipSuccess) return e;
         Workspace &w = st.ws[k];
@@ -2739,6 +2810,10 @@ static hipError_t get_state(uint32_t chunk, int nsets, DeviceState *&out)
         w.pqidx = (uint64_t *)p;
         p += align_up(n * kShakeSlots * kShakeRanks * sizeof(uint64_t));
         w.px = (uint32_t *)p;
+        p += align_up(n * 16 * sizeof(uint32_t));
+        w.defer = (uint32_t *)p;
+        p += align_up(n * kDeferPer * sizeof(uint32_t));
+        w.defer_cnt = (uint32_t *)p;
         st.ws_blocks[k] = chunk;
     }
     out = &st;
@@ -2756,6 +2831,10 @@ static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, h
     const uint32_t wg = 256;
     const uint32_t sm = p.stage_mask;
     const bool single = (sm & 0xCFu) != 0, dual = (sm & 0x30u) != 0;
+    // deferred shake problems of this pass (fast wave kernels -> slow ones);
+    // the slow kernels' grid: 4 waves per SIMD, striding over the lists
+    (void)hipMemsetAsync(ws.defer_cnt, 0, 4 * sizeof(uint32_t), s);
+    const dim3 slow_grid(512);
     if (single) {
         const uint64_t nq = (uint64_t)p.n * kQuantTasks;
         if (!integral) hipLaunchKernelGGL(k_quant, dim3((uint32_t)((nq + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
@@ -2793,6 +2872,11 @@ static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, h
             const uint64_t nw16 = (uint64_t)p.n * wave_count<16>(p.att) * 64;
             hipLaunchKernelGGL(k_shake_wave<16>, dim3((uint32_t)((nw16 + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
         }
+        if ((sm & 0x03u) && wave_count<8>(p.att))
+            hipLaunchKernelGGL(k_shake_wave_slow<8>, slow_grid, dim3(wg), 0, s, p, ws, sp);
+        if ((sm & 0x8Cu) && wave_count<4>(p.att))
+            hipLaunchKernelGGL(k_shake_wave_slow<4>, slow_grid, dim3(wg), 0, s, p, ws, sp);
+        if (sm & 0x40u) hipLaunchKernelGGL(k_shake_wave_slow<16>, slow_grid, dim3(wg), 0, s, p, ws, sp);
     }
     if (dual) {
         const uint64_t ndq = (uint64_t)p.n * kDualTasks * 2;
@@ -2804,6 +2888,7 @@ static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, h
         if (!integral) hipLaunchKernelGGL(k_dual, dim3((uint32_t)((nd + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
         const uint64_t ndw = (uint64_t)p.n * kDualTasks * 2 * 64;
         hipLaunchKernelGGL(k_dual_wave, dim3((uint32_t)((ndw + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
+        hipLaunchKernelGGL(k_dual_wave_slow, slow_grid, dim3(wg), 0, s, p, ws, sp);
     }
 }
 

@@ -58,6 +58,7 @@ static pthread_once_t g_once = PTHREAD_ONCE_INIT;
 /* instrumentation build only (search-shape statistics for kernel design) */
 unsigned long long orc_stats[9][48];
 static __thread int st_mode = 8;
+static __thread int st_integral_ = 0, st_mi0_ = 0;
 #define ST(i, v) __atomic_fetch_add(&orc_stats[st_mode][i], (unsigned long long)(v), __ATOMIC_RELAXED)
 #define ST_MODE(m) (st_mode = (m))
 #else
@@ -841,6 +842,28 @@ static void ls_endpoints(double data[][4], const int *cidx, int n, int last, int
         }
     }
     double dd = im[0][0] * im[1][1] - im[0][1] * im[0][1];
+#ifdef ORC_STATS
+    { /* exactly integral least-squares endpoints in [0, 255] (the GPU's integer table defers these) */
+        const long long a00 = (long long)im[0][0], a01 = (long long)im[0][1], a11 = (long long)im[1][1];
+        const long long d = a00 * a11 - a01 * a01;
+        for (int j = 0; j < dim; ++j)
+            for (int i = 0; i < 2; ++i) {
+                const long long xn = i ? -a01 : a11, yn = i ? a00 : -a01;
+                const long long nn = (xn * (long long)rp[0][j] + yn * (long long)rp[1][j]) * last;
+                if (d > 0 && nn % d == 0 && nn / d >= 0 && nn / d <= 255) {
+                    st_integral_ = 1; ST(43, 1);
+                    const double X = (i ? -im[0][1] : im[1][1]) / dd, Y = (i ? im[0][0] : -im[0][1]) / dd;
+                    const double v = (X * rp[0][j] + Y * rp[1][j]) * last;
+                    const double k = (double)(nn / d);
+                    if (nn == 0) ST(24, 1); else if (v == k) ST(25, 1); else if (v > k) ST(26, 1); else ST(27, 1);
+                    if (nn != 0 && rp[1][j] == 0) ST(28, 1);
+                    if (nn != 0 && rp[0][j] == 0) ST(29, 1);
+                    if (nn != 0 && v < k && (rp[0][j] == 0 || rp[1][j] == 0)) ST(30, 1);
+                }
+                ST(44, 1);
+            }
+    }
+#endif
     im[1][0] = im[0][0];
     im[0][0] = im[1][1] / dd;
     im[1][1] = im[1][0] / dd;
@@ -855,6 +878,9 @@ static void ls_endpoints(double data[][4], const int *cidx, int n, int last, int
 static double shake_window(double data[][4], int n, int *index_, int epo_code[2][4], int size, int last,
                            int bits, int dim)
 { ST(5, 1); ST(10, n);
+#ifdef ORC_STATS
+    st_integral_ = st_mi0_ = 0;
+#endif
     const int type = bits % (2 * dim);
     const int use_par = (type != 0);
     int mb[4];
@@ -878,6 +904,9 @@ static double shake_window(double data[][4], int n, int *index_, int epo_code[2]
 #endif
         ST(16 + (Mi < 15 ? Mi : 15), 0);
         if (Mi == 0) {
+#ifdef ORC_STATS
+            ST(46, 1);
+#endif
             double t;
             if (alls) {
                 t = single_point(data[0], n, index, outg, epo0, last, mb, type, dim);
@@ -1005,6 +1034,9 @@ static double shake_window(double data[][4], int n, int *index_, int epo_code[2]
         }
         done = !(change && better);
     } while (!done && max_try--);
+#ifdef ORC_STATS
+    ST(46, st_integral_);
+#endif
     return err_o;
 }
 
@@ -1013,6 +1045,10 @@ static double shake_window(double data[][4], int n, int *index_, int epo_code[2]
 static double shake_corners(double data[][4], int n, int *index_, int epo_code[2][4], int last,
                             const int *bits, int type, int dim)
 { ST(0, 1); ST(11, n);
+#ifdef ORC_STATS
+    st_integral_ = st_mi0_ = 0;
+    struct st_guard_ { int w; } stg_ = {0}; (void)stg_;
+#endif
     const int use_par = (type == PAR_BCC || type == PAR_SAME);
     const int bcc = (type == PAR_BCC);
     const int clog = clog_of(last), nc = 1 << clog;
@@ -1023,7 +1059,7 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
     mean_of(data, mean, n, dim);
 #ifdef ORC_STATS
     unsigned long long psig[512];
-    int npsig = 0;
+    int npsig = 0, st_dup_ = 0;
 #endif
     do {
         collapse(index, n);
@@ -1035,6 +1071,9 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
         int nsig = 0;
 #endif
         if (Mi == 0) {
+#ifdef ORC_STATS
+            ST(45, 1);
+#endif
             double t, o2[16][4];
             int epo0[2][4] = {{0}};
             if (alls) {
@@ -1096,9 +1135,11 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
                             for (int k = 0; k < npsig; ++k) dup |= psig[k] == ps;
                             ST(36, 1);
                             if (dup) ST(37, 1); else if (npsig < 512) psig[npsig++] = ps;
+                            st_dup_ = dup;
                         }
                         double te_[64][16];
                         const double thr_ = err1 < err2 ? err1 : err2;
+                        const double err1_in_ = err1;
 #endif
                         int s = 0;
                         for (int p1 = 0; p1 < 64; ++p1) {
@@ -1149,6 +1190,15 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
                                 for (int k = i; k > 0 && dm[ord[1][k]] > dm[ord[1][k - 1]]; --k) {
                                     int t = ord[1][k]; ord[1][k] = ord[1][k - 1]; ord[1][k - 1] = t;
                                 }
+                            { /* walked passes: does any corner end below thr (min needed), improve err1 */
+                                double mn = DBL_MAX;
+                                for (int c = 0; c < 64; ++c) {
+                                    double e = 0;
+                                    for (int i = 0; i < n; ++i) e += te_[c][i];
+                                    mn = e < mn ? e : mn;
+                                }
+                                if (!st_dup_) { ST(38, 1); ST(39, mn < thr_); ST(40, mn < err1_in_); }
+                            }
                             ST(32, 1); ST(35, n);
                             for (int o = 0; o < 2; ++o) {
                                 double part[64] = {0};
@@ -1194,6 +1244,9 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
         }
         done = !(change && better);
     } while (!done && max_try--);
+#ifdef ORC_STATS
+    ST(45, st_integral_);
+#endif
     return err_o;
 }
 
