@@ -134,8 +134,9 @@ def test_bc6h_unorm8_image(gpu):
 
 
 def test_bc6h_image_api(gpu):
-    """Image_CompressAMDBC6H: DXBC6H_UFLOAT for an RGBA float image (the
-    stand-in header marks R32G32B32A32_SFLOAT signed, so SFLOAT), bytes equal to
+    """Image_CompressAMDBC6H on an R32G32B32A32_SFLOAT image: the stand-in
+    header marks that format signed, so the destination is DXBC6H_SFLOAT (25)
+    and the signed encoder runs (amd_bc6h_compressor.cpp:19-25); bytes equal to
     the block path, a DDS with the DX10 header."""
     lib = gic.library()
     lib.Image_CreateNoClear.restype = ctypes.c_void_p
