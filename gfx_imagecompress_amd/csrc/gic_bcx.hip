@@ -110,13 +110,35 @@ __device__ __forceinline__ float ubyte_f(uint32_t w, int b)
     return r;
 }
 
+// LDS through its own address space (ds_read / ds_write).  The tables used to
+// be reached through volatile generic pointers to keep the compiler from
+// hoisting their loads into registers; volatile generic accesses compile to
+// flat loads with the cache-bypass bits, each followed by a vmcnt(0) wait (the
+// address-space inference leaves volatile accesses alone).  Now the address
+// goes through an empty asm at every use: as opaque to the optimiser, but an
+// ordinary LDS load the scheduler can batch.
+typedef __attribute__((address_space(3))) float lds_f32_t;
+typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
+__device__ __forceinline__ uint32_t lds_off(const void *p) { return (uint32_t)(uintptr_t)(const lds_f32_t *)p; }
+__device__ __forceinline__ float lds_ld_f(uint32_t a)
+{
+    asm volatile("" : "+v"(a));
+    return *(const lds_f32_t *)(size_t)a;
+}
+__device__ __forceinline__ uint32_t lds_ld_u(uint32_t a)
+{
+    asm volatile("" : "+v"(a));
+    return *(const lds_u32_t *)(size_t)a;
+}
+__device__ __forceinline__ void lds_st_u(uint32_t a, uint32_t v) { *(lds_u32_t *)(size_t)a = v; }
+
 struct ColB {
     uint32_t u[16];
     int n;
-    const volatile float *lut;   // LDS, 256 entries (volatile: re-read, not hoisted)
+    uint32_t lut;   // LDS byte address of the 256-entry byte -> v / 255.0f table
     __device__ __forceinline__ float c(int i, int ch) const { return ubyte_f(u[i], ch); }
     __device__ __forceinline__ float rpt(int i) const { return ubyte_f(u[i], 3); }
-    __device__ __forceinline__ float blk(int i, int ch) const { return lut[(u[i] >> (8 * ch)) & 255u]; }
+    __device__ __forceinline__ float blk(int i, int ch) const { return lds_ld_f(lut + 4u * ((u[i] >> (8 * ch)) & 255u)); }
 };
 struct ColF {
     float cc[16][3], r[16];
@@ -133,13 +155,16 @@ struct ColF {
 // register copy (regs()).
 constexpr int kLdsStride = 256;
 struct ColL {
-    volatile uint32_t *w;
+    uint32_t w;   // LDS byte address of this lane's colour 0
     int n;
-    const volatile float *lut;
-    __device__ __forceinline__ uint32_t word(int i) const { return w[i * kLdsStride]; }
+    uint32_t lut;
+    __device__ __forceinline__ uint32_t word(int i) const { return lds_ld_u(w + 4u * (uint32_t)(i * kLdsStride)); }
     __device__ __forceinline__ float c(int i, int ch) const { return ubyte_f(word(i), ch); }
     __device__ __forceinline__ float rpt(int i) const { return ubyte_f(word(i), 3); }
-    __device__ __forceinline__ float blk(int i, int ch) const { return lut[(word(i) >> (8 * ch)) & 255u]; }
+    __device__ __forceinline__ float blk(int i, int ch) const
+    {
+        return lds_ld_f(lut + 4u * ((word(i) >> (8 * ch)) & 255u));
+    }
     __device__ __forceinline__ ColB regs() const
     {
         ColB r;
@@ -914,7 +939,7 @@ __device__ __forceinline__ uint2 encode_bc1(const Col &u, int kept, const Tex &t
 
 template <bool R3D>
 __device__ __forceinline__ uint2 encode_bc1_u8(const uint32_t px[16], int steps, bool use_alpha, uint32_t thr_keep,
-                                               const TexG &t, const volatile float *lut)
+                                               const TexG &t, uint32_t lut)
 {
     ColB u;
     u.lut = lut;
@@ -926,7 +951,7 @@ __device__ __forceinline__ uint2 encode_bc1_u8(const uint32_t px[16], int steps,
 // the same with the colour words parked in LDS (ColL; w = this lane's column)
 template <bool R3D>
 __device__ __forceinline__ uint2 encode_bc1_u8_lds(const uint32_t px[16], int steps, bool use_alpha, uint32_t thr_keep,
-                                                   const TexG &t, const volatile float *lut, volatile uint32_t *w)
+                                                   const TexG &t, uint32_t lut, uint32_t w)
 {
     int kept;
     ColL ul;
@@ -935,7 +960,7 @@ __device__ __forceinline__ uint2 encode_bc1_u8_lds(const uint32_t px[16], int st
         u.lut = lut;
         unique_colours(u, px, use_alpha, thr_keep, kept);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) w[i * kLdsStride] = u.u[i];
+        for (int i = 0; i < 16; ++i) lds_st_u(w + 4u * (uint32_t)(i * kLdsStride), u.u[i]);
         ul.n = u.n;
     }
     ul.w = w;
@@ -1023,9 +1048,41 @@ __device__ __forceinline__ uint2 encode_explicit_alpha_f32(const float v[16])
 
 // ------------------------------------------------------------- BC4 ---
 
+// Storage of CompBlock1's compacted value / repeat arrays (uv, ur), written at
+// a running (data-dependent) position.  Private arrays indexed that way live
+// in scratch; the image kernels give each lane a column of LDS instead
+// (element k of lane t at k * 256 + t: consecutive lanes, consecutive banks).
+struct PrivArr {
+    float a[16];
+    __device__ __forceinline__ float &operator[](int k) { return a[k]; }
+    __device__ __forceinline__ float operator[](int k) const { return a[k]; }
+};
+struct LdsArr {
+    float *p;   // this lane's element 0
+    __device__ __forceinline__ float &operator[](int k) const { return p[k * 256]; }
+};
+// repeat counts (1..16) as bytes: a lane's 16 uv floats + 16 ur bytes = 80 B of LDS
+struct LdsCount {
+    uint8_t *p;
+    struct Ref {
+        uint8_t *q;
+        __device__ __forceinline__ operator float() const { return (float)*q; }
+        __device__ __forceinline__ Ref &operator=(float x) { *q = (uint8_t)x; return *this; }
+        __device__ __forceinline__ Ref &operator+=(float x) { *q = (uint8_t)((float)*q + x); return *this; }
+    };
+    __device__ __forceinline__ Ref operator[](int k) const { return Ref{p + k * 256}; }
+};
+struct Bc4Scratch {
+    PrivArr uv, ur;
+};
+struct Bc4Lds {
+    LdsArr uv;
+    LdsCount ur;
+};
+
 // RmpSrch1 evaluated in full, amd_bcx_body.cpp:1510-1548
-template <int N>
-__device__ __forceinline__ float scalar_ramp_error(const float *v, const float *rpt, float lo, float hi, int nv)
+template <int N, class A, class C>
+__device__ __forceinline__ float scalar_ramp_error(const A &v, const C &rpt, float lo, float hi, int nv)
 {
     float error = 0;
     const float step = (hi - lo) / (float)(N - 1);
@@ -1040,16 +1097,17 @@ __device__ __forceinline__ float scalar_ramp_error(const float *v, const float *
         else
             q = (floorf((del + step_h) * rstep) * step) + lo;
         const float d = v[i] - q;
-        error += d * d * rpt[i];
+        error += d * d * (float)rpt[i];
     }
     return error;
 }
 
 // CompBlock1 (8-bit integer grid), amd_bcx_body.cpp:1633-1832
-template <int N, bool FIXED>
-__device__ void scalar_endpoints(float ramp[2], const float vals_sorted[16])
+template <int N, bool FIXED, class W>
+__device__ void scalar_endpoints(float ramp[2], const float vals_sorted[16], W &wk)
 {
-    float uv[16], ur[16];
+    auto &uv = wk.uv;
+    auto &ur = wk.ur;
     int nu = 0;
     bool need = true;
     float prev = -2.f;
@@ -1195,11 +1253,11 @@ __device__ float scalar_cluster(const float v[16], float ramp[2], uint64_t &ibit
     return err;
 }
 
-template <int N, bool FIXED>
-__device__ float scalar_block(const float v[16], const float sorted[16], uint8_t ep[2], uint64_t &ibits)
+template <int N, bool FIXED, class W>
+__device__ float scalar_block(const float v[16], const float sorted[16], uint8_t ep[2], uint64_t &ibits, W &wk)
 {
     float ramp[2];
-    scalar_endpoints<N, FIXED>(ramp, sorted);
+    scalar_endpoints<N, FIXED>(ramp, sorted, wk);
     const float err = scalar_cluster<N, FIXED>(v, ramp, ibits);
     ep[0] = (uint8_t)ramp[0];
     ep[1] = (uint8_t)ramp[1];
@@ -1208,7 +1266,8 @@ __device__ float scalar_block(const float v[16], const float sorted[16], uint8_t
 
 // Image_CompressAMDAlphaSingleModeBlock + EncodeAlphaBlock,
 // amd_bcx_helpers.cpp:32-46, :125-140
-__device__ uint64_t encode_bc4(const float v[16])
+template <class W = Bc4Scratch>
+__device__ uint64_t encode_bc4(const float v[16], W wk = W())
 {
     // ascending sort by rank (equal values are interchangeable)
     float s[16];
@@ -1250,9 +1309,9 @@ __device__ uint64_t encode_bc4(const float v[16])
     }
     uint8_t ep8[2], ep6[2];
     uint64_t i8, i6 = 0;
-    const float e8 = scalar_block<8, false>(v, s, ep8, i8);
+    const float e8 = scalar_block<8, false>(v, s, ep8, i8, wk);
     float e6 = 3.402823466e+38f;
-    if (!(e8 == 0.f)) e6 = scalar_block<6, true>(v, s, ep6, i6);
+    if (!(e8 == 0.f)) e6 = scalar_block<6, true>(v, s, ep6, i6, wk);
     const bool use8 = e8 <= e6;
     const uint8_t *ep = use8 ? ep8 : ep6;
     return (uint64_t)ep[0] | ((uint64_t)ep[1] << 8) | ((use8 ? i8 : i6) << 16);
@@ -1283,7 +1342,8 @@ __global__ void __launch_bounds__(256, 3) bc1_image_kernel(Geometry g, Bc1Params
     uint32_t px[16];
     load_block_u8(g, slice, by, bx, p.force_alpha_one != 0, px);
     const bcx::TexG t{g, id, p.force_alpha_one != 0, p.thr_final};
-    dst[id] = bcx::encode_bc1_u8_lds<R3D>(px, p.steps, p.alpha_threshold > 0.0f, p.thr_keep, t, lut, cols + threadIdx.x);
+    dst[id] = bcx::encode_bc1_u8_lds<R3D>(px, p.steps, p.alpha_threshold > 0.0f, p.thr_keep, t, bcx::lds_off(lut),
+                                          bcx::lds_off(cols + threadIdx.x));
 }
 
 // BC2 / BC3 (amd_bc2_compressor.cpp:36-50, amd_bc3_compressor.cpp:36-50): alpha
@@ -1314,7 +1374,7 @@ __global__ void __launch_bounds__(256, 2) bc23_image_kernel(Geometry g, int fmt,
         a = bcx::encode_explicit_alpha_u8(px);
     }
     bcx::ColB u;
-    u.lut = lut;
+    u.lut = bcx::lds_off(lut);
     int kept;
     bcx::unique_colours(u, px, false, 0u, kept);
     const bcx::TexB t{px, 0u};
@@ -1322,26 +1382,39 @@ __global__ void __launch_bounds__(256, 2) bc23_image_kernel(Geometry g, int fmt,
     dst[id] = make_uint4(a.x, a.y, c.x, c.y);
 }
 
-__global__ void __launch_bounds__(256) bc45_image_kernel(Geometry g, int fmt, int channel,
-                                                         uint64_t *__restrict__ dst)
+// BC4 (one channel) / BC5 (channels 0 and 1) over an 8-bit image: the block's
+// texels as packed bytes (row loads of 4 / 8 / 16 bytes for 1 / 2 / 4
+// channels), each selected byte to v / 255.0f through a 256-entry LDS table.
+// (A float RGBA gather indexed by a runtime channel went to scratch: 608 bytes
+// per lane.)
+template <int FMT>
+__global__ void __launch_bounds__(256) bc45_image_kernel(Geometry g, int channel, uint64_t *__restrict__ dst)
 {
+    __shared__ float lut[256];   // byte -> v / 255.0f
+    __shared__ float wk_uv[16 * 256];     // CompBlock1's uv of each lane
+    __shared__ uint8_t wk_ur[16 * 256];   // and its repeat counts
+    lut[threadIdx.x] = (float)threadIdx.x / 255.0f;
+    __syncthreads();
     const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
     if (id >= g.total) return;
     uint32_t slice, by, bx;
     block_coords(g, id, slice, by, bx);
-    float blk[64], v[16];
-    load_block(g, slice, by, bx, false, blk);
-    if (fmt == 4) {
+    uint32_t px[16];
+    load_block_u8(g, slice, by, bx, false, px);
+    const bcx::Bc4Lds wk{{wk_uv + threadIdx.x}, {wk_ur + threadIdx.x}};
+    float v[16];
+    if (FMT == 4) {
+        const uint32_t sh = 8u * (uint32_t)channel;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = blk[i * 4 + channel];
-        dst[id] = bcx::encode_bc4(v);
+        for (int i = 0; i < 16; ++i) v[i] = lut[(px[i] >> sh) & 255u];
+        dst[id] = bcx::encode_bc4(v, wk);
     } else {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = blk[i * 4 + 0];
-        const uint64_t r = bcx::encode_bc4(v);
+        for (int i = 0; i < 16; ++i) v[i] = lut[px[i] & 255u];
+        const uint64_t r = bcx::encode_bc4(v, wk);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = blk[i * 4 + 1];
-        const uint64_t gch = bcx::encode_bc4(v);
+        for (int i = 0; i < 16; ++i) v[i] = lut[(px[i] >> 8) & 255u];
+        const uint64_t gch = bcx::encode_bc4(v, wk);
         dst[2 * (size_t)id] = r;
         dst[2 * (size_t)id + 1] = gch;
     }
@@ -1666,7 +1739,10 @@ hipError_t launch_bc23_blocks(const float *blocks, uint32_t n, int fmt, int step
 hipError_t launch_bc45_image(const Geometry &g, int fmt, int channel, void *dst, hipStream_t s)
 {
     const uint32_t wg = 256, grid = (g.total + wg - 1) / wg;
-    hipLaunchKernelGGL(bc45_image_kernel, dim3(grid), dim3(wg), 0, s, g, fmt, channel, (uint64_t *)dst);
+    if (fmt == 4)
+        hipLaunchKernelGGL(bc45_image_kernel<4>, dim3(grid), dim3(wg), 0, s, g, channel, (uint64_t *)dst);
+    else
+        hipLaunchKernelGGL(bc45_image_kernel<5>, dim3(grid), dim3(wg), 0, s, g, channel, (uint64_t *)dst);
     return hipGetLastError();
 }
 

@@ -101,6 +101,26 @@ __device__ __forceinline__ void load_block_u8(const Geometry &g, uint32_t slice,
             out[y * 4 + 2] = row.z;
             out[y * 4 + 3] = row.w;
         }
+    } else if (g.channels == 1 && x0 + 4 <= g.width && y0 + 4 <= g.height && (g.row_pitch & 3) == 0 &&
+               ((uintptr_t)g.src & 3) == 0) {
+        // R8: one 4-byte load per row
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+            const uint32_t row = *reinterpret_cast<const uint32_t *>(img + (size_t)(y0 + y) * g.row_pitch + x0);
+#pragma unroll
+            for (int x = 0; x < 4; ++x) out[y * 4 + x] = (row >> (8 * x)) & 0xffu;
+        }
+    } else if (g.channels == 2 && x0 + 4 <= g.width && y0 + 4 <= g.height && (g.row_pitch & 7) == 0 &&
+               ((uintptr_t)g.src & 7) == 0) {
+        // R8G8: one 8-byte load per row
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+            const uint2 row = *reinterpret_cast<const uint2 *>(img + (size_t)(y0 + y) * g.row_pitch + x0 * 2);
+            out[y * 4 + 0] = row.x & 0xffffu;
+            out[y * 4 + 1] = row.x >> 16;
+            out[y * 4 + 2] = row.y & 0xffffu;
+            out[y * 4 + 3] = row.y >> 16;
+        }
     } else {
 #pragma unroll
         for (int y = 0; y < 4; ++y) {

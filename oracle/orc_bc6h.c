@@ -400,6 +400,9 @@ static float ramp8(int clog, int p1, int p2, int i)
 /* ep_shaker_HD, amd_hdr_encode.cpp:2280-2614, dimension 3, bits {8, 8, 8}
  * (use_par 0), Mi_ = numEntries - 1.  maxTry starts at 1 and is decremented
  * before the loop test, so exactly one round runs. */
+#ifdef ORC_STATS
+unsigned long long orc_bc6h_stats[4];
+#endif
 static float shaker_hd(float data[][4], int n, int *index_, int epo_code[2][4])
 {
     const int Mi_ = n - 1;
@@ -447,6 +450,18 @@ static float shaker_hd(float data[][4], int n, int *index_, int epo_code[2][4])
     int p0 = -1, q0 = -1;
     float err_2 = FLT_MAX;
     int idx_2[16], epo_2[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#ifdef ORC_STATS
+    /* instrumentation build only: shaker calls, expansions, texel-corner work */
+    {
+        extern unsigned long long orc_bc6h_stats[4];
+        __atomic_fetch_add(&orc_bc6h_stats[0], 1ull, __ATOMIC_RELAXED);
+        unsigned long long ne = 0;
+        for (int q = 1; q * Mi <= Mi_; q++) ne += (unsigned long long)(Mi_ - q * Mi + 1);
+        __atomic_fetch_add(&orc_bc6h_stats[1], ne, __ATOMIC_RELAXED);
+        __atomic_fetch_add(&orc_bc6h_stats[2], ne * 64ull * (unsigned long long)n, __ATOMIC_RELAXED);
+        __atomic_fetch_add(&orc_bc6h_stats[3], Mi == 1 ? 1ull : 0ull, __ATOMIC_RELAXED);
+    }
+#endif
     for (int q = 1; q * Mi <= Mi_; q++)
         for (int p = 0; p <= Mi_ - q * Mi; p++) {
             int cidx[16];
