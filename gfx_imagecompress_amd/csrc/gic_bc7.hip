@@ -63,6 +63,7 @@ constexpr int kDualTasks = 12;     // mode 4: 4 rot x 2 sel, mode 5: 4 rot
 constexpr int kUMax = 496;
 __constant__ uint32_t dUProb[kUMax];      // mask | log2(clusters) << 16
 __constant__ uint32_t dUMinPart[kUMax];   // byte m: lowest partition of mode m using it, 0xFF = none
+__constant__ uint32_t dUMask[kUMax];      // distinct masks: u (8 clusters) | u (4 clusters) << 16, 0xFFFF = none
 __constant__ uint16_t dTaskSub[208][3];   // task (modes 0-3) x subset -> problem, 0xFFFF = no subset
 __constant__ int kSlotMode[6] = {0, 1, 2, 3, 6, 7};
 __constant__ int kSlotBase[6] = {0, 16, 80, 144, 208, 209};
@@ -1484,28 +1485,38 @@ __global__ void __launch_bounds__(256) k_quant(Params p, Workspace ws)
 // of modes 0-3's subset problems), so each distinct one is solved once and
 // k_quant_gather sums the per-partition errors in subset order, exactly as the
 // per-partition loop of CompressSingleIndexBlock (:582-641) does.
-// Grid: x = subset problem u (wave-uniform), y = 256-block group, lane = block.
+// Grid: x = distinct subset mask (wave-uniform), y = 256-block group, lane =
+// block.  A mask used with 8 clusters (modes 0, 1) and with 4 (modes 2, 3) is
+// two problems over the same texels: their mean, covariance and principal
+// vector (quant_prefix) are computed once and both quantisations run from it.
 // Every lane of a wave solves the same subset shape, so its texels are loaded
 // compacted (slot k = the k-th member) and every member loop of the quantiser
 // runs exactly n iterations under uniform branches (SelPrefix) -- a lane per
 // (block, problem) paid all 16 texel slots of every loop with per-lane masks.
 // Consecutive workgroups share their 256 blocks' texels in cache.
-__global__ void __launch_bounds__(256, 2) k_quant_sub(Params p, Workspace ws)
+__device__ __forceinline__ bool subset_needed(const BlockMeta &meta, const Params &p, uint32_t u)
 {
-    const int u = (int)blockIdx.x;
-    const uint32_t b = blockIdx.y * blockDim.x + threadIdx.x;
-    if (b >= p.n) return;
-    const BlockMeta meta = ws.meta[b];
-    if ((meta.flags & 3u) != 2u) return;
+    if (u == 0xFFFFu) return false;
     const uint32_t mp = dUMinPart[u];
     bool need = false;
     for (int m = 0; m < 4; ++m) {
         const uint32_t mpart = (mp >> (8 * m)) & 0xFFu;
         need = need || (mpart != 0xFFu && mode_active(meta, p, m) && (int)mpart < mode_tries(p, m));
     }
-    if (!need) return;
-    const uint32_t pr = dUProb[u];
-    const uint32_t mask = pr & 0xFFFFu;
+    return need;
+}
+
+__global__ void __launch_bounds__(256, 2) k_quant_sub(Params p, Workspace ws)
+{
+    const uint32_t pair = dUMask[blockIdx.x];
+    const uint32_t b = blockIdx.y * blockDim.x + threadIdx.x;
+    if (b >= p.n) return;
+    const BlockMeta meta = ws.meta[b];
+    if ((meta.flags & 3u) != 2u) return;
+    const uint32_t u8 = pair & 0xFFFFu, u4 = pair >> 16;
+    const bool need8 = subset_needed(meta, p, u8), need4 = subset_needed(meta, p, u4);
+    if (!need8 && !need4) return;
+    const uint32_t mask = dUProb[u8 != 0xFFFFu ? u8 : u4] & 0xFFFFu;
     const int n = __popc(mask);
     const float *tex = ws.tex + (size_t)b * 64;
     uint32_t px[16];
@@ -1522,21 +1533,29 @@ __global__ void __launch_bounds__(256, 2) k_quant_sub(Params p, Workspace ws)
             }
         }
     }
-    int idx[16];
-    const double err = opt_quant_sel<3>(px, SelPrefix{n}, 1 << (pr >> 16), idx);
-    uint64_t tidx = 0;
-    {
-        uint32_t m = mask;
+    double mean[4] = {0, 0, 0, 0}, dir[4];
+    const bool spread = quant_prefix<3>(px, SelPrefix{n}, mean, dir);
+#pragma unroll 1
+    for (int pass = 0; pass < 2; ++pass) {
+        if (!(pass == 0 ? need8 : need4)) continue;
+        const uint32_t u = pass == 0 ? u8 : u4;
+        int idx[16];
+        double err = 0.;
+        uint64_t tidx = 0;
+        if (spread) {
+            err = opt_quant_from<3>(px, SelPrefix{n}, pass == 0 ? 8 : 4, idx, mean, dir);
+            uint32_t m = mask;
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
-            if (k < n) {
-                const int t = __builtin_ctz(m);
-                m &= m - 1;
-                tidx |= (uint64_t)(idx[k] & 15) << (4 * t);
-            }
+            for (int k = 0; k < 16; ++k)
+                if (k < n) {
+                    const int t = __builtin_ctz(m);
+                    m &= m - 1;
+                    tidx |= (uint64_t)(idx[k] & 15) << (4 * t);
+                }
+        }
+        ws.uerr[(size_t)b * kUMax + u] = err;
+        ws.uidx[(size_t)b * kUMax + u] = tidx;
     }
-    ws.uerr[(size_t)b * kUMax + u] = err;
-    ws.uidx[(size_t)b * kUMax + u] = tidx;
 }
 
 // K1b: per-partition errors and indices of modes 0-3 from the subset problems
@@ -1988,7 +2007,7 @@ __device__ __forceinline__ void defer_push(const Params &p, const Workspace &ws,
 }
 
 // waves per SIMD of the fast kernels (<= 72 / 64 / 80 VGPRs, no spills)
-template <int NC> struct ShakeOcc { static constexpr int v = 7; };
+template <int NC> struct ShakeOcc { static constexpr int v = 8; };
 template <> struct ShakeOcc<4> { static constexpr int v = 8; };
 template <> struct ShakeOcc<16> { static constexpr int v = 6; };   // 16 ramp points per corner lane
 template <int NC> constexpr int shake_kind() { return NC == 8 ? 0 : (NC == 4 ? 1 : 2); }
@@ -2550,7 +2569,25 @@ static int build_subset_problems(std::vector<uint32_t> &prob, std::vector<uint32
         }
     return (int)prob.size();
 }
-static int g_nu = 0;
+// the problems paired by mask (k_quant_sub's grid x)
+static int build_subset_masks(const std::vector<uint32_t> &prob, std::vector<uint32_t> &pairs)
+{
+    pairs.clear();
+    std::vector<uint32_t> masks;
+    for (size_t u = 0; u < prob.size(); ++u) {
+        const uint32_t mask = prob[u] & 0xFFFFu;
+        const bool eight = (prob[u] >> 16) == 3u;
+        size_t i = 0;
+        while (i < masks.size() && masks[i] != mask) ++i;
+        if (i == masks.size()) {
+            masks.push_back(mask);
+            pairs.push_back(0xFFFFFFFFu);
+        }
+        pairs[i] = eight ? (pairs[i] & 0xFFFF0000u) | (uint32_t)u : (pairs[i] & 0xFFFFu) | ((uint32_t)u << 16);
+    }
+    return (int)pairs.size();
+}
+static int g_nu = 0, g_nm = 0;
 
 // traceBuilder (amd_bc7_3dquant_vpc.cpp:1557-1712) for ne entries and nc
 // clusters, appended to kc/d.  Seven nested loops (one per delimiter, each
@@ -2740,11 +2777,15 @@ static hipError_t get_state(uint32_t chunk, int nsets, DeviceState *&out)
         if (e == hipSuccess)
             e = hipMemcpyToSymbol(HIP_SYMBOL(dUMinPart), minpart.data(), minpart.size() * sizeof(uint32_t));
         if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dTaskSub), tsub.data(), tsub.size() * sizeof(uint16_t));
+        std::vector<uint32_t> pairs;
+        const int nm = build_subset_masks(prob, pairs);
+        if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dUMask), pairs.data(), pairs.size() * sizeof(uint32_t));
         if (e != hipSuccess) {
             (void)hipFree(sp);
             return e;
         }
         g_nu = nu;
+        g_nm = nm;
         st.device = dev;
         st.sp = sp;
     }
@@ -2832,15 +2873,15 @@ static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, h
     const uint32_t sm = p.stage_mask;
     const bool single = (sm & 0xCFu) != 0, dual = (sm & 0x30u) != 0;
     // deferred shake problems of this pass (fast wave kernels -> slow ones);
-    // the slow kernels' grid: 4 waves per SIMD, striding over the lists
+    // the slow kernels' grid: 4 waves per SIMD (their VGPRs allow 4), striding over the lists
     (void)hipMemsetAsync(ws.defer_cnt, 0, 4 * sizeof(uint32_t), s);
-    const dim3 slow_grid(512);
+    const dim3 slow_grid(1024);
     if (single) {
         const uint64_t nq = (uint64_t)p.n * kQuantTasks;
         if (!integral) hipLaunchKernelGGL(k_quant, dim3((uint32_t)((nq + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
         const uint64_t nq3 = (uint64_t)p.n * 208, nq4 = (uint64_t)p.n * 65;
         if (sm & 0x0Fu) {
-            hipLaunchKernelGGL(k_quant_sub, dim3((uint32_t)g_nu, (p.n + wg - 1) / wg), dim3(wg), 0, s, p, ws);
+            hipLaunchKernelGGL(k_quant_sub, dim3((uint32_t)g_nm, (p.n + wg - 1) / wg), dim3(wg), 0, s, p, ws);
             hipLaunchKernelGGL(k_quant_gather, dim3((uint32_t)((nq3 + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
         }
         if ((sm & 0xC0u) == 0x40u && p.probe) {   // the bounded exit's mode-6 probe: first projection only

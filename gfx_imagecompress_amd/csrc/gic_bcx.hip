@@ -125,10 +125,13 @@ __device__ __forceinline__ float lds_ld_f(uint32_t a)
     asm volatile("" : "+v"(a));
     return *(const lds_f32_t *)(size_t)a;
 }
-__device__ __forceinline__ uint32_t lds_ld_u(uint32_t a)
+// base made opaque, the constant offset added after it (the ds_read offset
+// field): an opaque base + offset address would be computed for every word up
+// front and kept live -- the 3-wave BC1 build spilled those addresses
+__device__ __forceinline__ uint32_t lds_ld_u(uint32_t base, uint32_t off)
 {
-    asm volatile("" : "+v"(a));
-    return *(const lds_u32_t *)(size_t)a;
+    asm volatile("" : "+v"(base));
+    return *(const lds_u32_t *)(size_t)(base + off);
 }
 __device__ __forceinline__ void lds_st_u(uint32_t a, uint32_t v) { *(lds_u32_t *)(size_t)a = v; }
 
@@ -158,7 +161,7 @@ struct ColL {
     uint32_t w;   // LDS byte address of this lane's colour 0
     int n;
     uint32_t lut;
-    __device__ __forceinline__ uint32_t word(int i) const { return lds_ld_u(w + 4u * (uint32_t)(i * kLdsStride)); }
+    __device__ __forceinline__ uint32_t word(int i) const { return lds_ld_u(w, 4u * (uint32_t)(i * kLdsStride)); }
     __device__ __forceinline__ float c(int i, int ch) const { return ubyte_f(word(i), ch); }
     __device__ __forceinline__ float rpt(int i) const { return ubyte_f(word(i), 3); }
     __device__ __forceinline__ float blk(int i, int ch) const
@@ -815,6 +818,23 @@ struct TexG {
     }
 };
 
+// The block's texels parked in LDS (this lane's column, lane-contiguous rows
+// as ColL) for the final clustering.  Re-reading them from the image (TexG)
+// kept the block's 64-bit source addresses alive through the search, and the
+// 3-wave build spilled those to scratch: ~64 B of scratch traffic per block.
+struct TexL {
+    uint32_t a;   // LDS byte address of this lane's texel 0
+    uint32_t thr_final;
+    __device__ __forceinline__ TexV view() const
+    {
+        TexV v;
+        v.thr_final = thr_final;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v.px[i] = lds_ld_u(a, 4u * (uint32_t)(i * kLdsStride));
+        return v;
+    }
+};
+
 // Clstr -> ClstrBas -> ClstrIntnl, amd_bcx_body.cpp:258-378
 template <int N, class Tex>
 __device__ __forceinline__ uint32_t final_indices(const Tex &tex, const uint8_t ep[3][2], bool use_alpha, float &err)
@@ -949,9 +969,9 @@ __device__ __forceinline__ uint2 encode_bc1_u8(const uint32_t px[16], int steps,
 }
 
 // the same with the colour words parked in LDS (ColL; w = this lane's column)
-template <bool R3D>
+template <bool R3D, class Tex>
 __device__ __forceinline__ uint2 encode_bc1_u8_lds(const uint32_t px[16], int steps, bool use_alpha, uint32_t thr_keep,
-                                                   const TexG &t, uint32_t lut, uint32_t w)
+                                                   const Tex &t, uint32_t lut, uint32_t w)
 {
     int kept;
     ColL ul;
@@ -1333,6 +1353,7 @@ __global__ void __launch_bounds__(256, 3) bc1_image_kernel(Geometry g, Bc1Params
 {
     __shared__ float lut[256];   // byte -> v / 255.0f
     __shared__ uint32_t cols[16 * bcx::kLdsStride];   // ColL words of the workgroup's lanes
+    __shared__ uint32_t texs[16 * bcx::kLdsStride];   // and their blocks' texels (TexL)
     lut[threadIdx.x] = (float)threadIdx.x / 255.0f;
     __syncthreads();
     const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1341,7 +1362,10 @@ __global__ void __launch_bounds__(256, 3) bc1_image_kernel(Geometry g, Bc1Params
     block_coords(g, id, slice, by, bx);
     uint32_t px[16];
     load_block_u8(g, slice, by, bx, p.force_alpha_one != 0, px);
-    const bcx::TexG t{g, id, p.force_alpha_one != 0, p.thr_final};
+    const uint32_t ta = bcx::lds_off(texs + threadIdx.x);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) bcx::lds_st_u(ta + 4u * (uint32_t)(i * bcx::kLdsStride), px[i]);
+    const bcx::TexL t{ta, p.thr_final};
     dst[id] = bcx::encode_bc1_u8_lds<R3D>(px, p.steps, p.alpha_threshold > 0.0f, p.thr_keep, t, bcx::lds_off(lut),
                                           bcx::lds_off(cols + threadIdx.x));
 }

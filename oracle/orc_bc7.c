@@ -56,7 +56,7 @@ static double g_sp_err[3][4][256][2][2][16];
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
 #ifdef ORC_STATS
 /* instrumentation build only (search-shape statistics for kernel design) */
-unsigned long long orc_stats[9][48];
+unsigned long long orc_stats[9][64];
 static __thread int st_mode = 8;
 static __thread int st_integral_ = 0, st_mi0_ = 0;
 #define ST(i, v) __atomic_fetch_add(&orc_stats[st_mode][i], (unsigned long long)(v), __ATOMIC_RELAXED)
@@ -1198,6 +1198,31 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
                                     mn = e < mn ? e : mn;
                                 }
                                 if (!st_dup_) { ST(38, 1); ST(39, mn < thr_); ST(40, mn < err1_in_); }
+                            }
+                            if (!st_dup_) { /* walked passes: texels under the natural, distance and min-contribution orders */
+                                int ord3[16];
+                                double mc[16];
+                                for (int i = 0; i < n; ++i) {
+                                    ord3[i] = i;
+                                    mc[i] = DBL_MAX;
+                                    for (int c = 0; c < 64; ++c) mc[i] = te_[c][i] < mc[i] ? te_[c][i] : mc[i];
+                                }
+                                for (int i = 1; i < n; ++i)
+                                    for (int k = i; k > 0 && mc[ord3[k]] > mc[ord3[k - 1]]; --k) {
+                                        int t = ord3[k]; ord3[k] = ord3[k - 1]; ord3[k - 1] = t;
+                                    }
+                                const int *oo[3] = {ord[0], ord[1], ord3};
+                                ST(48, n);
+                                for (int o = 0; o < 3; ++o) {
+                                    double part[64] = {0};
+                                    int used = n;
+                                    for (int m = 0; m < n; ++m) {
+                                        int all = 1;
+                                        for (int c = 0; c < 64; ++c) { part[c] += te_[c][oo[o][m]]; all &= part[c] >= thr_; }
+                                        if ((m & 1) && all) { used = m + 1; break; }
+                                    }
+                                    ST(49 + o, used);
+                                }
                             }
                             ST(32, 1); ST(35, n);
                             for (int o = 0; o < 2; ++o) {

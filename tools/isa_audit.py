@@ -11,7 +11,12 @@ Extracts the device code objects of lib/libgfx_imagecompress_amd.so
     The kernels must have none;
   * scalar-cache writes (s_store / s_buffer_store / s_scratch_store / scalar
     atomics / s_dcache_wb), which this project never emits;
-  * scratch (private segment) use, reported for information.
+  * scratch (private segment) use, reported for information;
+  * per-kernel resources from the code objects' metadata notes (VGPRs,
+    SGPRs, their spill counts, private and LDS bytes, waves per SIMD the
+    VGPR count allows) and the v_writelane_b32 count of each kernel (SGPR
+    spill stores go through v_writelane into a VGPR lane, reloads through
+    v_readlane).
 Usage: python tools/isa_audit.py [lib.so]   -> exit 1 on a finding.
 """
 from __future__ import annotations
@@ -26,6 +31,7 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "gfx_imagecompress_amd", "lib", "libgfx_imagecompress_amd.so")
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
 
 _FUNC = re.compile(r"^[0-9a-f]+ <(\S+)>:$")
 _RFL = re.compile(r"v_readfirstlane_b32 s(\d+), v")
@@ -51,9 +57,42 @@ def disassemble(lib: str) -> list[str]:
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def resources(lib: str) -> dict:
+    """{kernel symbol: {vgpr, sgpr, vgpr_spill, sgpr_spill, private, lds, waves}}
+    from the gfx950 code objects' AMDGPU metadata notes."""
+    tmp = tempfile.mkdtemp(prefix="gic_res_")
+    out = {}
+    try:
+        dst = os.path.join(tmp, "lib.so")
+        shutil.copy(lib, dst)
+        subprocess.run([OBJDUMP, "--offloading", dst], cwd=tmp, check=True, capture_output=True)
+        for f in sorted(os.listdir(tmp)):
+            if "amdgcn" not in f or "gfx950" not in f:
+                continue
+            notes = subprocess.run([READELF, "--notes", os.path.join(tmp, f)], check=True, capture_output=True,
+                                   text=True).stdout
+            for m in re.split(r"\n\s+- \.agpr_count", notes):
+                nm = re.search(r"\.symbol:\s+(\S+)\.kd", m)
+                if not nm:
+                    continue
+
+                def g(k):
+                    mm = re.search(re.escape(k) + r":\s+(\d+)", m)
+                    return int(mm.group(1)) if mm else 0
+                v = g(".vgpr_count")
+                out[nm.group(1)] = {"vgpr": v, "sgpr": g(".sgpr_count"), "vgpr_spill": g(".vgpr_spill_count"),
+                                    "sgpr_spill": g(".sgpr_spill_count"),
+                                    "private": g(".private_segment_fixed_size"),
+                                    "lds": g(".group_segment_fixed_size"),
+                                    "waves": min(8, 512 // max(8, (v + 7) // 8 * 8))}
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    return out
+
+
 def audit(lines: list[str]) -> dict:
     """{'uniform_loads': [(kernel, text)], 'scalar_stores': [...], 'scratch': {kernel: count}, 'kernels': n}"""
-    res = {"uniform_loads": [], "scalar_stores": [], "scratch": {}, "kernels": 0}
+    res = {"uniform_loads": [], "scalar_stores": [], "scratch": {}, "kernels": 0, "writelane": {}}
     kern = "?"
     for i, line in enumerate(lines):
         m = _FUNC.match(line)
@@ -65,6 +104,8 @@ def audit(lines: list[str]) -> dict:
             res["scalar_stores"].append((kern, line.split("//")[0].strip()))
         if _SCRATCH.search(line):
             res["scratch"][kern] = res["scratch"].get(kern, 0) + 1
+        if "v_writelane_b32" in line:
+            res["writelane"][kern] = res["writelane"].get(kern, 0) + 1
         m = _RFL.search(line)
         if not m:
             continue
@@ -89,6 +130,12 @@ def main() -> int:
     print(f"{res['kernels']} device functions")
     for k, n in sorted(res["scratch"].items(), key=lambda kv: -kv[1]):
         print(f"  scratch ops {n:6d}  {k[:100]}")
+    rs = resources(lib)
+    print("kernel resources (VGPRs, waves/SIMD by VGPRs, spills, private/LDS bytes, v_writelane count):")
+    for k, r in sorted(rs.items()):
+        print(f"  vgpr {r['vgpr']:3d} ({r['waves']} w)  sgpr {r['sgpr']:3d}  vspill {r['vgpr_spill']:3d}  "
+              f"sspill {r['sgpr_spill']:4d}  priv {r['private']:4d}  lds {r['lds']:6d}  "
+              f"writelane {res['writelane'].get(k, 0):4d}  {k[:90]}")
     for kind in ("uniform_loads", "scalar_stores"):
         for k, t in res[kind]:
             print(f"FINDING {kind}: {k[:80]}: {t}")

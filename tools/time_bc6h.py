@@ -19,9 +19,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--only", choices=["signed", "unsigned"], default=None)
     a = ap.parse_args()
     n = a.size
     for signed in (False, True):
+        if a.only and (a.only == "signed") != signed:
+            continue
         img = synth.hdr_rgba(n, n, seed=1, signed=signed)
         src = torch.from_numpy(img.reshape(-1).copy()).cuda()
         nb = (n // 4) ** 2
