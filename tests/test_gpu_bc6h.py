@@ -171,3 +171,19 @@ def test_bc6h_image_api(gpu):
         assert raw[148:] == data
     lib.Image_Destroy(q)
     lib.Image_Destroy(p)
+
+
+def test_bc6h_gpu_blocks_decode_independently(gpu):
+    """The kernels' own blocks read by the format-description decoder
+    (tests/bc6h_decode.py; tests/test_bc6h_decode.py holds the reasoning):
+    unsigned blocks decode to texels whose error is the kernels' reported
+    block error within one unit per channel value."""
+    import bc6h_decode as D
+    from test_bc6h_decode import _half_int, _input_half_int
+    blocks = np.concatenate([_tile_blocks(synth.hdr_rgba(64, 32, seed=5)), _random_blocks(128, 13)])
+    got, gerr = _gpu_blocks(blocks)
+    for k in range(len(got)):
+        d = D.decode_block(got[k], False)
+        assert 1 <= d["mode"] <= 10, (k, d["mode"])
+        dec = np.abs(_input_half_int(blocks[k], False) - _half_int(d["texels"].view(np.float16))).sum()
+        assert abs(dec - gerr[k]) <= 48, (k, d["mode"], dec, gerr[k])
