@@ -2098,31 +2098,60 @@ __device__ __forceinline__ void dual_task(uint32_t task, int &mode, int &rot, in
     sel = task < 8 ? (int)(task & 1) : 0;
 }
 
+// One lane per (block, rotation, half): the three candidates of a rotation
+// (mode 4 selections 0 and 1, mode 5) quantise the same texels of a half with
+// 4 or 8 clusters, so the lane computes the quantiser prefix (mean, covariance,
+// principal vector) once and each distinct cluster count once, and writes
+// every active candidate's slot -- 24 quantiser runs per block become <= 16,
+// 24 prefixes 8.
 __global__ void __launch_bounds__(256, 2) k_dual_quant_reg(Params p, Workspace ws)
 {
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t b = gid / (kDualTasks * 2), r = gid % (kDualTasks * 2);
+    const uint32_t b = gid >> 3, rot = (gid >> 1) & 3u, half = gid & 1u;
     if (b >= p.n) return;
-    const uint32_t task = r >> 1, half = r & 1;
-    int mode, rot, sel;
-    dual_task(task, mode, rot, sel);
     const BlockMeta meta = ws.meta[b];
-    if (!mode_active(meta, p, mode) || (meta.flags & 3u) != 2u) return;
-    const ModeInfo &mi = kModes[mode];
-    const int ncl = 1 << dual_index_bits(mi, (int)half, sel);
+    if ((meta.flags & 3u) != 2u) return;
+    const bool act4 = mode_active(meta, p, 4), act5 = mode_active(meta, p, 5);
+    if (!act4 && !act5) return;
+    // the rotation's tasks: mode 4 selection 0, mode 4 selection 1, mode 5
+    const uint32_t tk0 = 2 * rot, tk1 = 2 * rot + 1, tk2 = 8 + rot;
+    const int n0 = 1 << dual_index_bits(kModes[4], (int)half, 0), n1 = 1 << dual_index_bits(kModes[4], (int)half, 1),
+              n2 = 1 << dual_index_bits(kModes[5], (int)half, 0);
     const float *tex = ws.tex + (size_t)b * 64;
     const int c0 = kRot[rot][half ? 0 : 1], c1 = kRot[rot][half ? 0 : 2], c2 = kRot[rot][half ? 0 : 3];
     uint32_t px[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i)
         px[i] = (uint32_t)tex[i * 4 + c0] | ((uint32_t)tex[i * 4 + c1] << 8) | ((uint32_t)tex[i * 4 + c2] << 16);
-    int idx[16];
-    const double qe = opt_quant_mask<3>(px, 0xffffu, ncl, idx);
-    uint64_t ti = 0;
+    double mean[4] = {0, 0, 0, 0}, dir[4];
+    const bool spread = quant_prefix<3>(px, SelPrefix{16}, mean, dir);
+#pragma unroll 1
+    for (int pass = 0; pass < 2; ++pass) {
+        const int ncl = pass ? 8 : 4;
+        const bool w0 = act4 && n0 == ncl, w1 = act4 && n1 == ncl, w2 = act5 && n2 == ncl;
+        if (!(w0 || w1 || w2)) continue;
+        double qe = 0.;
+        uint64_t ti = 0;
+        if (spread) {
+            int idx[16];
+            qe = opt_quant_from<3>(px, SelPrefix{16}, ncl, idx, mean, dir);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) ti |= (uint64_t)(idx[k] & 15) << (4 * k);
-    ws.dqidx[((size_t)b * kDualTasks + task) * 2 + half] = ti;
-    ws.dqerr[((size_t)b * kDualTasks + task) * 2 + half] = qe;
+            for (int k = 0; k < 16; ++k) ti |= (uint64_t)(idx[k] & 15) << (4 * k);
+        }
+        const size_t base = (size_t)b * kDualTasks;
+        if (w0) {
+            ws.dqidx[(base + tk0) * 2 + half] = ti;
+            ws.dqerr[(base + tk0) * 2 + half] = qe;
+        }
+        if (w1) {
+            ws.dqidx[(base + tk1) * 2 + half] = ti;
+            ws.dqerr[(base + tk1) * 2 + half] = qe;
+        }
+        if (w2) {
+            ws.dqidx[(base + tk2) * 2 + half] = ti;
+            ws.dqerr[(base + tk2) * 2 + half] = qe;
+        }
+    }
 }
 
 __global__ void __launch_bounds__(256) k_dual_quant(Params p, Workspace ws)
@@ -2922,7 +2951,8 @@ static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, h
     if (dual) {
         const uint64_t ndq = (uint64_t)p.n * kDualTasks * 2;
         if (!integral) hipLaunchKernelGGL(k_dual_quant, dim3((uint32_t)((ndq + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
-        hipLaunchKernelGGL(k_dual_quant_reg, dim3((uint32_t)((ndq + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
+        const uint64_t ndr = (uint64_t)p.n * 8;   // (block, rotation, half)
+        hipLaunchKernelGGL(k_dual_quant_reg, dim3((uint32_t)((ndr + wg - 1) / wg)), dim3(wg), 0, s, p, ws);
         if (p.quant_thr < 255.0)
             hipLaunchKernelGGL(k_dual_quant_trace, dim3((uint32_t)((ndq + 63) / 64)), dim3(64), 0, s, p, ws);
         const uint64_t nd = (uint64_t)p.n * kDualTasks;
