@@ -1506,18 +1506,34 @@ __device__ __forceinline__ bool subset_needed(const BlockMeta &meta, const Param
     return need;
 }
 
-__global__ void __launch_bounds__(256, 2) k_quant_sub(Params p, Workspace ws)
+// QcDiv's offsets from a workgroup table in LDS (address made opaque at every
+// read, so the loads stay at the use instead of being hoisted into VGPRs)
+struct QcLds {
+    uint32_t a;
+    __device__ __forceinline__ double at(int q, int) const
+    {
+        uint32_t b = a;
+        asm volatile("" : "+v"(b));
+        return *(const __attribute__((address_space(3))) double *)(size_t)(b + 8u * (uint32_t)q);
+    }
+};
+
+__global__ void __launch_bounds__(256, 3) k_quant_sub(Params p, Workspace ws)
 {
+    __shared__ double qc_tab[16];
     const uint32_t pair = dUMask[blockIdx.x];
+    const uint32_t u8 = pair & 0xFFFFu, u4 = pair >> 16;
+    const uint32_t mask = dUProb[u8 != 0xFFFFu ? u8 : u4] & 0xFFFFu;
+    const int n = __popc(mask);
+    if (threadIdx.x < 16) qc_tab[threadIdx.x] = QcDiv{}.at((int)threadIdx.x, n);
+    __syncthreads();
+    const QcLds qc{(uint32_t)(uintptr_t)(const __attribute__((address_space(3))) double *)qc_tab};
     const uint32_t b = blockIdx.y * blockDim.x + threadIdx.x;
     if (b >= p.n) return;
     const BlockMeta meta = ws.meta[b];
     if ((meta.flags & 3u) != 2u) return;
-    const uint32_t u8 = pair & 0xFFFFu, u4 = pair >> 16;
     const bool need8 = subset_needed(meta, p, u8), need4 = subset_needed(meta, p, u4);
     if (!need8 && !need4) return;
-    const uint32_t mask = dUProb[u8 != 0xFFFFu ? u8 : u4] & 0xFFFFu;
-    const int n = __popc(mask);
     const float *tex = ws.tex + (size_t)b * 64;
     uint32_t px[16];
     {
@@ -1543,7 +1559,7 @@ __global__ void __launch_bounds__(256, 2) k_quant_sub(Params p, Workspace ws)
         double err = 0.;
         uint64_t tidx = 0;
         if (spread) {
-            err = opt_quant_from<3>(px, SelPrefix{n}, pass == 0 ? 8 : 4, idx, mean, dir);
+            err = opt_quant_from<3>(px, SelPrefix{n}, pass == 0 ? 8 : 4, idx, mean, dir, qc);
             uint32_t m = mask;
 #pragma unroll
             for (int k = 0; k < 16; ++k)
@@ -2106,6 +2122,10 @@ __device__ __forceinline__ void dual_task(uint32_t task, int &mode, int &rot, in
 // 24 prefixes 8.
 __global__ void __launch_bounds__(256, 2) k_dual_quant_reg(Params p, Workspace ws)
 {
+    __shared__ double qc_tab[16];
+    if (threadIdx.x < 16) qc_tab[threadIdx.x] = QcDiv{}.at((int)threadIdx.x, 16);
+    __syncthreads();
+    const QcLds qc{(uint32_t)(uintptr_t)(const __attribute__((address_space(3))) double *)qc_tab};
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t b = gid >> 3, rot = (gid >> 1) & 3u, half = gid & 1u;
     if (b >= p.n) return;
@@ -2134,7 +2154,7 @@ __global__ void __launch_bounds__(256, 2) k_dual_quant_reg(Params p, Workspace w
         uint64_t ti = 0;
         if (spread) {
             int idx[16];
-            qe = opt_quant_from<3>(px, SelPrefix{16}, ncl, idx, mean, dir);
+            qe = opt_quant_from<3>(px, SelPrefix{16}, ncl, idx, mean, dir, qc);
 #pragma unroll
             for (int k = 0; k < 16; ++k) ti |= (uint64_t)(idx[k] & 15) << (4 * k);
         }

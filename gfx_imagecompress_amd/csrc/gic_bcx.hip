@@ -136,6 +136,7 @@ __device__ __forceinline__ uint32_t lds_ld_u(uint32_t base, uint32_t off)
 __device__ __forceinline__ void lds_st_u(uint32_t a, uint32_t v) { *(lds_u32_t *)(size_t)a = v; }
 
 struct ColB {
+    static constexpr bool kRefine3 = false;
     uint32_t u[16];
     int n;
     uint32_t lut;   // LDS byte address of the 256-entry byte -> v / 255.0f table
@@ -144,6 +145,7 @@ struct ColB {
     __device__ __forceinline__ float blk(int i, int ch) const { return lds_ld_f(lut + 4u * ((u[i] >> (8 * ch)) & 255u)); }
 };
 struct ColF {
+    static constexpr bool kRefine3 = false;
     float cc[16][3], r[16];
     int n;
     __device__ __forceinline__ float c(int i, int ch) const { return cc[i][ch]; }
@@ -157,7 +159,12 @@ struct ColF {
 // every use re-reads, nothing is hoisted into registers.  Refine takes a
 // register copy (regs()).
 constexpr int kLdsStride = 256;
-struct ColL {
+// S1: the kernel runs only RefinementSteps == 1 (the default), and Refine
+// takes refine_pass3 alone -- with the general pass compiled in beside it the
+// 3-wave kernel spilled (see refine_pass3)
+template <bool S1>
+struct ColLT {
+    static constexpr bool kRefine3 = S1;
     uint32_t w;   // LDS byte address of this lane's colour 0
     int n;
     uint32_t lut;
@@ -180,7 +187,8 @@ struct ColL {
 };
 __device__ __forceinline__ const ColB &regs(const ColB &u) { return u; }
 __device__ __forceinline__ const ColF &regs(const ColF &u) { return u; }
-__device__ __forceinline__ ColB regs(const ColL &u) { return u.regs(); }
+template <bool S1>
+__device__ __forceinline__ ColB regs(const ColLT<S1> &u) { return u.regs(); }
 
 // ClstrErr (weighted), amd_bcx_body.cpp:214-255
 template <int N, class Col>
@@ -267,6 +275,85 @@ __device__ __forceinline__ void refine_pass(float cur[3][2], const float base[3]
     cur[CH][1] = b1;
 }
 
+// The same pass for steps == 1 (the default: a, b in {-1, 0, 1}) over the
+// LDS-parked colours (ColL), loops swapped: the nine candidates' ramps are
+// built first, then one sweep over the block's colours -- a rolled loop, one
+// LDS word per colour, n iterations -- accumulates all nine errors (each still
+// summed in colour order; colours past n add +0), and the first strictly
+// smaller candidate in (a, b) order wins as before.  Only one colour's N side
+// terms are live instead of all 16 x N, which pushed the 3-wave BC1 kernel
+// into scratch spills (32 B written per block).
+template <int N, int CH>
+__device__ __forceinline__ void refine_pass3(float cur[3][2], const float base[3][2], const ColLT<true> &u,
+                                             float &best)
+{
+    const float wr = 0.3086f, wg = 0.6094f, wb = 0.0820f;
+    float wk[3][2], r[3][4];
+    {
+        const bool flat = expand_grid(wk, cur);
+        (void)flat;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) chan_ramp<N>(r[c], wk[c]);
+    }
+    const float grid = (float)(1 << (8 - chan_bits(CH)));
+    const float wc = (CH == CH_R) ? wr : (CH == CH_G) ? wg : wb;
+    float rc[9][4], e0[9], e1[9], mse[9];
+    bool flt[9];
+#pragma unroll
+    for (int ab = 0; ab < 9; ++ab) {
+        const int a = ab / 3 - 1, b = ab % 3 - 1;
+        cur[CH][0] = minr(maxr(base[CH][0] + (float)a * grid, 0.f), 255.f);
+        cur[CH][1] = minr(maxr(base[CH][1] + (float)b * grid, 0.f), 255.f);
+        e0[ab] = cur[CH][0];
+        e1[ab] = cur[CH][1];
+        flt[ab] = expand_grid(wk, cur);
+        chan_ramp<N>(rc[ab], wk[CH]);
+        mse[ab] = 0.f;
+    }
+#pragma unroll 1
+    for (int i = 0; i < u.n; ++i) {
+        const uint32_t wd = u.word(i);
+        const float cr = ubyte_f(wd, CH_R), cg = ubyte_f(wd, CH_G), cb = ubyte_f(wd, CH_B), rp = ubyte_f(wd, 3);
+        float side[4];
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            if (CH == CH_R) {
+                float dg = r[CH_G][k] - cg, db = r[CH_B][k] - cb;
+                side[k] = dg * dg * wg + db * db * wb;
+            } else if (CH == CH_G) {
+                float dr = r[CH_R][k] - cr, db = r[CH_B][k] - cb;
+                side[k] = dr * dr * wr + db * db * wb;
+            } else {
+                float dr = r[CH_R][k] - cr, dg = r[CH_G][k] - cg;
+                side[k] = dr * dr * wr + dg * dg * wg;
+            }
+        }
+        const float ci = CH == CH_R ? cr : (CH == CH_G ? cg : cb);
+#pragma unroll
+        for (int ab = 0; ab < 9; ++ab) {
+            float m = 10000000.f;
+            const int nr = flt[ab] ? 1 : N;
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                float d = rc[ab][k] - ci;
+                float e = side[k] + d * d * wc;
+                m = (k < nr) ? minr(m, e) : m;
+            }
+            mse[ab] += m * rp;
+        }
+    }
+    float b0 = base[CH][0], b1 = base[CH][1];
+#pragma unroll
+    for (int ab = 0; ab < 9; ++ab)
+        if (mse[ab] < best) {
+            b0 = e0[ab];
+            b1 = e1[ab];
+            best = mse[ab];
+        }
+    cur[CH][0] = b0;
+    cur[CH][1] = b1;
+}
+
 template <int N, class Col>
 __device__ __forceinline__ void refine_channels(float cur[3][2], const Col &u, int steps)
 {
@@ -279,12 +366,21 @@ __device__ __forceinline__ void refine_channels(float cur[3][2], const Col &u, i
     const bool flat = expand_grid(wk, cur);
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) chan_ramp<N>(r[ch], wk[ch]);
-    float best = ramp_fit_error<N>(u, r, flat);
+    float best = ramp_fit_error<N>(regs(u), r, flat);
     if (best == 0.f || !steps) return;
     const int lo = -(int)minr((float)steps, 8.f), hi = (int)minr((float)steps, 8.f);
-    refine_pass<N, CH_R>(cur, base, u, lo, hi, best);
-    refine_pass<N, CH_G>(cur, base, u, lo, hi, best);
-    refine_pass<N, CH_B>(cur, base, u, lo, hi, best);
+    if constexpr (Col::kRefine3) {   // steps == 1 (the kernel's precondition)
+        (void)lo;
+        (void)hi;
+        refine_pass3<N, CH_R>(cur, base, u, best);
+        refine_pass3<N, CH_G>(cur, base, u, best);
+        refine_pass3<N, CH_B>(cur, base, u, best);
+    } else {
+        const auto &ur = regs(u);
+        refine_pass<N, CH_R>(cur, base, ur, lo, hi, best);
+        refine_pass<N, CH_G>(cur, base, ur, lo, hi, best);
+        refine_pass<N, CH_B>(cur, base, ur, lo, hi, best);
+    }
 }
 
 // Refine3D, amd_bcx_body.cpp:808-932 (b3DRefinement): the joint jitter of all
@@ -641,11 +737,10 @@ __device__ __forceinline__ void fit_endpoints(float result[3][2], const Col &u, 
             for (int j = 0; j < 3; ++j) rc[j][k] = (pos_g[k] * dir_g[j] + mid[j]) * 255.f;
     }
     snap_grid(result, rc);
-    const auto &ur = regs(u);
     if (R3D)
-        refine_3d<N>(result, ur, steps);
+        refine_3d<N>(result, regs(u), steps);
     else
-        refine_channels<N>(result, ur, steps);
+        refine_channels<N>(result, u, steps);
 }
 
 // Leaders and ranks of the kept texels' colour keys: a kept texel leads its
@@ -969,12 +1064,12 @@ __device__ __forceinline__ uint2 encode_bc1_u8(const uint32_t px[16], int steps,
 }
 
 // the same with the colour words parked in LDS (ColL; w = this lane's column)
-template <bool R3D, class Tex>
+template <bool R3D, bool S1, class Tex>
 __device__ __forceinline__ uint2 encode_bc1_u8_lds(const uint32_t px[16], int steps, bool use_alpha, uint32_t thr_keep,
                                                    const Tex &t, uint32_t lut, uint32_t w)
 {
     int kept;
-    ColL ul;
+    ColLT<S1> ul;
     {
         ColB u;
         u.lut = lut;
@@ -1348,7 +1443,7 @@ struct Bc1Params {
     uint32_t thr_keep, thr_final;   // alpha-byte forms of the two threshold tests
 };
 
-template <bool R3D>
+template <bool R3D, bool S1>
 __global__ void __launch_bounds__(256, 3) bc1_image_kernel(Geometry g, Bc1Params p, uint2 *__restrict__ dst)
 {
     __shared__ float lut[256];   // byte -> v / 255.0f
@@ -1366,7 +1461,7 @@ __global__ void __launch_bounds__(256, 3) bc1_image_kernel(Geometry g, Bc1Params
 #pragma unroll
     for (int i = 0; i < 16; ++i) bcx::lds_st_u(ta + 4u * (uint32_t)(i * bcx::kLdsStride), px[i]);
     const bcx::TexL t{ta, p.thr_final};
-    dst[id] = bcx::encode_bc1_u8_lds<R3D>(px, p.steps, p.alpha_threshold > 0.0f, p.thr_keep, t, bcx::lds_off(lut),
+    dst[id] = bcx::encode_bc1_u8_lds<R3D, S1>(px, p.steps, p.alpha_threshold > 0.0f, p.thr_keep, t, bcx::lds_off(lut),
                                           bcx::lds_off(cols + threadIdx.x));
 }
 
@@ -1731,9 +1826,11 @@ hipError_t launch_bc1_image(const Geometry &g, float thr, int steps, int force_a
     const Bc1Params p{thr, steps, force_alpha_one, keep, fin};
     const uint32_t wg = 256, grid = (g.total + wg - 1) / wg;
     if (r3d)
-        hipLaunchKernelGGL(bc1_image_kernel<true>, dim3(grid), dim3(wg), 0, s, g, p, (uint2 *)dst);
+        hipLaunchKernelGGL((bc1_image_kernel<true, false>), dim3(grid), dim3(wg), 0, s, g, p, (uint2 *)dst);
+    else if (steps == 1)
+        hipLaunchKernelGGL((bc1_image_kernel<false, true>), dim3(grid), dim3(wg), 0, s, g, p, (uint2 *)dst);
     else
-        hipLaunchKernelGGL(bc1_image_kernel<false>, dim3(grid), dim3(wg), 0, s, g, p, (uint2 *)dst);
+        hipLaunchKernelGGL((bc1_image_kernel<false, false>), dim3(grid), dim3(wg), 0, s, g, p, (uint2 *)dst);
     return hipGetLastError();
 }
 

@@ -78,3 +78,19 @@ def test_bc4_bc5_image_kernels_use_no_scratch(res):
     for part in ("bc45_image_kernelILi4E", "bc45_image_kernelILi5E"):
         r = _kernel(res, part)
         assert r["private"] == 0 and r["vgpr_spill"] == 0, (part, r)
+
+
+def test_bc1_default_kernel_runs_three_waves_without_scratch(res):
+    """RefinementSteps == 1 (the default) has its own BC1 kernel whose Refine
+    sweeps the LDS-parked colours once per candidate set (refine_pass3): no
+    scratch, so the kernel's HBM traffic is the texels in and the blocks out
+    (profiles/traffic_bc1.json)."""
+    r = _kernel(res, "bc1_image_kernelILb0ELb1E")
+    assert r["waves"] >= 3 and r["private"] == 0 and r["vgpr_spill"] == 0, r
+
+
+def test_quant_sub_runs_three_waves(res):
+    """k_quant_sub (f64 quantiser, latency bound) fits 3 waves per SIMD with
+    the indices packed in bytes and the lattice offsets in LDS."""
+    r = _kernel(res, "k_quant_subE")
+    assert r["waves"] >= 3 and r["private"] <= 64, r
