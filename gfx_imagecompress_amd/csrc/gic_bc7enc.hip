@@ -88,9 +88,30 @@ struct Res {            // color_cell_compressor_results :297-305
     uint64_t sel;       // selector of texel i in nibble i (texels of the subset only)
 };
 
-// per-texel transforms of the perceptual metric, computed once per block
+// per-texel transforms of the perceptual metric, computed once per block and
+// parked in the workgroup's LDS (rows l 0..15, cr 16..31, cb 32..47, each row
+// 256 lanes wide, so a wave's reads are conflict-free).  Held in registers
+// they were 48 VGPRs live through the whole search (2 waves per SIMD); the
+// read address is opaque at every use so the loads stay inside the ramp loops.
+constexpr uint32_t kYccStride = 256;
 struct Ycc {
-    int l[16], cr[16], cb[16];
+    uint32_t a;   // LDS byte address of this lane's row-0 word
+    __device__ __forceinline__ int at(int row) const
+    {
+        uint32_t b = a;
+        asm volatile("" : "+v"(b));
+        return *(const __attribute__((address_space(3))) int *)(size_t)(b + 4u * (uint32_t)row * kYccStride);
+    }
+    __device__ __forceinline__ int l(int i) const { return at(i); }
+    __device__ __forceinline__ int cr(int i) const { return at(16 + i); }
+    __device__ __forceinline__ int cb(int i) const { return at(32 + i); }
+    __device__ __forceinline__ void put(int i, int l_, int cr_, int cb_) const
+    {
+        typedef __attribute__((address_space(3))) int lds_i32;
+        *(lds_i32 *)(size_t)(a + 4u * (uint32_t)i * kYccStride) = l_;
+        *(lds_i32 *)(size_t)(a + 4u * (uint32_t)(16 + i) * kYccStride) = cr_;
+        *(lds_i32 *)(size_t)(a + 4u * (uint32_t)(32 + i) * kYccStride) = cb_;
+    }
 };
 
 // scale_color :307-323 (n = component bits + p-bit)
@@ -247,7 +268,7 @@ __device__ __forceinline__ void evaluate(const uint32_t lo[K], const uint32_t hi
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     const int d = a1 - (int)ch(tex(px, i), 3);
-                    const uint32_t e = ycc_err(l1[0], cr1[0], cb1[0], tx.l[i], tx.cr[i], tx.cb[i], cf,
+                    const uint32_t e = ycc_err(l1[0], cr1[0], cb1[0], tx.l(i), tx.cr(i), tx.cb(i), cf,
                                                mad24(mul24(w3, d), d, 0));
                     key[i] = min(key[i], (e << 4) | j);
                 }
@@ -256,7 +277,7 @@ __device__ __forceinline__ void evaluate(const uint32_t lo[K], const uint32_t hi
                 for (int i = 0; i < 16; ++i) {
                     const bool f0 = first_subset<K>(m0, i);
                     const uint32_t e = ycc_err(f0 ? l1[0] : l1[K - 1], f0 ? cr1[0] : cr1[K - 1],
-                                               f0 ? cb1[0] : cb1[K - 1], tx.l[i], tx.cr[i], tx.cb[i], cf);
+                                               f0 ? cb1[0] : cb1[K - 1], tx.l(i), tx.cr(i), tx.cb(i), cf);
                     key[i] = min(key[i], (e << 4) | j);
                 }
             }
@@ -464,7 +485,7 @@ __device__ __forceinline__ void one_colour(uint32_t cr, uint32_t cg, uint32_t cb
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const uint32_t c = tex(px, i);
-        const uint32_t e = P ? ycc_err(ql, qcr, qcb, tx.l[i], tx.cr[i], tx.cb[i], cf)
+        const uint32_t e = P ? ycc_err(ql, qcr, qcb, tx.l(i), tx.cr(i), tx.cb(i), cf)
                              : wsq(q[0] - (int)ch(c, 0), q[1] - (int)ch(c, 1), q[2] - (int)ch(c, 2), cf);
         const bool in = (pr.mask >> i) & 1u;
         tot += in ? e : 0u;
@@ -793,7 +814,7 @@ __device__ __forceinline__ uint32_t estimate2(uint32_t m0, const uint32_t px[16]
         if (P) {
             int l1, cr1, cb1;
             ycc(c[0], c[1], c[2], l1, cr1, cb1);
-            tot += ycc_err(l1, cr1, cb1, tx.l[i], tx.cr[i], tx.cb[i], cf);
+            tot += ycc_err(l1, cr1, cb1, tx.l(i), tx.cr(i), tx.cb(i), cf);
         } else {
             tot += wsq(c[0] - (int)ch(tex(px, i), 0), c[1] - (int)ch(tex(px, i), 1), c[2] - (int)ch(tex(px, i), 2), cf);
         }
@@ -903,12 +924,15 @@ __device__ __forceinline__ uint4 pack_block(bool mode1, uint32_t part, uint64_t 
 // :1390-1515 (m_endpoints_share_pbit, uninitialised for alpha blocks in the
 // reference, is false: mode 6 has a p-bit per endpoint)
 template <bool P>
-__device__ __forceinline__ uint4 encode_block(const uint32_t px[16], const EncCfg &cf, const EncLds &L)
+__device__ __forceinline__ uint4 encode_block(const uint32_t px[16], const EncCfg &cf, const EncLds &L, Ycc tx)
 {
-    Ycc tx;
     if (P) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) ycc(ch(tex(px, i), 0), ch(tex(px, i), 1), ch(tex(px, i), 2), tx.l[i], tx.cr[i], tx.cb[i]);
+        for (int i = 0; i < 16; ++i) {
+            int l, cr, cb;
+            ycc(ch(tex(px, i), 0), ch(tex(px, i), 1), ch(tex(px, i), 2), l, cr, cb);
+            tx.put(i, l, cr, cb);
+        }
     }
     bool alpha = false;
 #pragma unroll
@@ -953,9 +977,14 @@ __device__ __forceinline__ uint4 encode_block(const uint32_t px[16], const EncCf
 
 // ---- kernels ---------------------------------------------------------------
 
-// waves per SIMD the kernels are register-budgeted for (build-time override for studies)
+// waves per SIMD the kernels are register-budgeted for (build-time override for
+// studies).  3: with the perceptual transforms in LDS the 3-wave build spills
+// only values read once per block (the PCA endpoints, the cfg); 8K G1 uber 4
+// perceptual 32.8 -> 32.0 ms, uber 0 12.9 -> 12.2 ms, RGB metric 20.0 -> 18.0 ms
+// and 11.2 -> 10.3 ms against the 2-wave build, same blocks
+// (profiles/r04c_bc7enc_ab.txt)
 #ifndef GIC_ENC_WAVES
-#define GIC_ENC_WAVES 2
+#define GIC_ENC_WAVES 3
 #endif
 
 __device__ __forceinline__ void load_tables(EncLds &L)
@@ -973,14 +1002,16 @@ __global__ void __launch_bounds__(256, GIC_ENC_WAVES) bc7enc_image_kernel(Geomet
                                                            uint4 *__restrict__ dst)
 {
     __shared__ EncLds L;
+    __shared__ int ytab[P ? 48 * kYccStride : 1];
     load_tables(L);
+    const Ycc tx{(uint32_t)(uintptr_t)(const __attribute__((address_space(3))) int *)(ytab + (P ? threadIdx.x : 0))};
     const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
     if (id >= g.total) return;
     uint32_t slice, by, bx;
     block_coords(g, id, slice, by, bx);
     uint32_t px[16];
     load_block_u8(g, slice, by, bx, force_alpha_one != 0, px);
-    dst[id] = encode_block<P>(px, cf, L);
+    dst[id] = encode_block<P>(px, cf, L, tx);
 }
 
 // Image_CompressRichGel999BC7enc16 :73-97: blocks of 16 packed RGBA8 words
@@ -989,7 +1020,9 @@ __global__ void __launch_bounds__(256, GIC_ENC_WAVES) bc7enc_blocks_kernel(const
                                                             uint4 *__restrict__ dst)
 {
     __shared__ EncLds L;
+    __shared__ int ytab[P ? 48 * kYccStride : 1];
     load_tables(L);
+    const Ycc tx{(uint32_t)(uintptr_t)(const __attribute__((address_space(3))) int *)(ytab + (P ? threadIdx.x : 0))};
     const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
     if (id >= n) return;
     uint32_t px[16];
@@ -998,7 +1031,7 @@ __global__ void __launch_bounds__(256, GIC_ENC_WAVES) bc7enc_blocks_kernel(const
         const uint4 v = blocks[(size_t)id * 4 + q];
         px[q * 4 + 0] = v.x, px[q * 4 + 1] = v.y, px[q * 4 + 2] = v.z, px[q * 4 + 3] = v.w;
     }
-    dst[id] = encode_block<P>(px, cf, L);
+    dst[id] = encode_block<P>(px, cf, L, tx);
 }
 
 // float RGBA blocks (the gic_hip_encode_rows_src / block-ABI path): each texel
@@ -1009,7 +1042,9 @@ __global__ void __launch_bounds__(256, GIC_ENC_WAVES) bc7enc_f32_kernel(const fl
                                                          uint4 *__restrict__ dst)
 {
     __shared__ EncLds L;
+    __shared__ int ytab[P ? 48 * kYccStride : 1];
     load_tables(L);
+    const Ycc tx{(uint32_t)(uintptr_t)(const __attribute__((address_space(3))) int *)(ytab + (P ? threadIdx.x : 0))};
     const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
     if (id >= n) return;
     uint32_t px[16];
@@ -1023,7 +1058,7 @@ __global__ void __launch_bounds__(256, GIC_ENC_WAVES) bc7enc_f32_kernel(const fl
         for (int k = 0; k < 4; ++k) w |= (uint32_t)(sat(c[k]) * 255.0f + 0.5f) << (8 * k);
         px[t] = w;
     }
-    dst[id] = encode_block<P>(px, cf, L);
+    dst[id] = encode_block<P>(px, cf, L, tx);
 }
 
 EncCfg make_cfg(const gic_options &o)

@@ -29,3 +29,8 @@ names = {0: "c.collapse", 1: "c.ls", 2: "c.pass_setup", 3: "c.build_ramp", 4: "c
 tot = sum(buf[i] for i in names)
 for i, nm in names.items():
     print(f"{nm:16s} {buf[i] / 1e9:10.3f} Gcyc {100.0 * buf[i] / tot:6.1f}%")
+counts = {22: "corner passes walked", 23: "corner texel pairs", 24: "corner passes cut", 25: "corner passes deduped",
+          26: "corner expansions", 27: "corner texels of walked passes", 28: "corner passes skipping the min",
+          29: "corners() calls"}
+for i, nm in counts.items():
+    print(f"{nm:32s} {buf[i]:14d}")

@@ -21,4 +21,7 @@ for fast, perc in ((False, True), (True, True), (False, False), (True, False)):
     e.record()
     torch.cuda.synchronize()
     ms = s.elapsed_time(e) / 3
-    print(f"fast={fast} perceptual={perc}: {ms:.2f} ms  {n * n / ms / 1e3:.1f} Mpix/s", flush=True)
+    import hashlib
+    dig = hashlib.sha1(dst.cpu().numpy().tobytes()).hexdigest()[:16]
+    print(f"{os.environ.get('GIC_LIBRARY', '')} fast={fast} perceptual={perc}: {ms:.2f} ms  "
+          f"{n * n / ms / 1e3:.1f} Mpix/s  digest {dig}", flush=True)
