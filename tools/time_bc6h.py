@@ -40,8 +40,10 @@ def main():
         e1.record(s)
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / a.reps
-        print(f"BC6H {'signed' if signed else 'unsigned'} {n}x{n}: {ms:.1f} ms = {n * n / ms / 1e3:.2f} Mpix/s, "
-              f"{nb / ms * 1e3:.0f} blocks/s", flush=True)
+        import hashlib
+        dig = hashlib.sha1(dst.cpu().numpy().tobytes()).hexdigest()[:16]
+        print(f"{os.environ.get('GIC_LIBRARY', '')} BC6H {'signed' if signed else 'unsigned'} {n}x{n}: {ms:.1f} ms = "
+              f"{n * n / ms / 1e3:.2f} Mpix/s, {nb / ms * 1e3:.0f} blocks/s  digest {dig}", flush=True)
 
 
 if __name__ == "__main__":
