@@ -888,19 +888,44 @@ static thread_local int t_block_status = GIC_OK;
 
 extern "C" int gic_block_last_status(void) { return t_block_status; }
 
+// One block's input and output in mapped pinned host memory: the kernels read
+// the 64 floats and write the block words across PCIe themselves, so a call is
+// a memcpy into the stage, the launches and one stream synchronisation -- no
+// DMA copies in either direction (each pageable hipMemcpy was a staged copy of
+// its own with a wait).
+struct BlockStage {
+    float *h_in = nullptr;
+    uint8_t *h_out = nullptr;
+    void *d_in = nullptr, *d_out = nullptr;
+    ~BlockStage()
+    {
+        if (h_in) (void)hipHostFree(h_in);
+        if (h_out) (void)hipHostFree(h_out);
+    }
+    bool ready()
+    {
+        if (d_in && d_out) return true;
+        if (!h_in && hipHostMalloc((void **)&h_in, 64 * sizeof(float), hipHostMallocMapped) != hipSuccess) return false;
+        if (!h_out && hipHostMalloc((void **)&h_out, 64, hipHostMallocMapped) != hipSuccess) return false;
+        return hipHostGetDevicePointer(&d_in, h_in, 0) == hipSuccess &&
+               hipHostGetDevicePointer(&d_out, h_out, 0) == hipSuccess;
+    }
+};
+static thread_local BlockStage t_stage;
+
 static bool encode_one_block(gic_format fmt, const float *in, size_t nfloats, const gic_options &o, void *out,
                              size_t out_bytes)
 {
     DeviceScratch &s = t_scratch;
+    BlockStage &b = t_stage;
     int st = GIC_OK;
-    if (!s.reserve(nfloats * sizeof(float), out_bytes) ||
-        hipMemcpyAsync(s.src, in, nfloats * sizeof(float), hipMemcpyHostToDevice, s.stream) != hipSuccess)
-        st = GIC_EHIP;
-    if (st == GIC_OK)
-        st = gic_hip_encode_blocks_f32(fmt, (const float *)s.src, 1, &o, (uint8_t *)s.dst, nullptr, s.stream);
-    if (st == GIC_OK && (hipMemcpyAsync(out, s.dst, out_bytes, hipMemcpyDeviceToHost, s.stream) != hipSuccess ||
-                         hipStreamSynchronize(s.stream) != hipSuccess))
-        st = GIC_EHIP;
+    if (nfloats > 64 || out_bytes > 64 || !s.reserve(0, 0) || !b.ready()) st = GIC_EHIP;
+    if (st == GIC_OK) {
+        memcpy(b.h_in, in, nfloats * sizeof(float));
+        st = gic_hip_encode_blocks_f32(fmt, (const float *)b.d_in, 1, &o, (uint8_t *)b.d_out, nullptr, s.stream);
+    }
+    if (st == GIC_OK && hipStreamSynchronize(s.stream) != hipSuccess) st = GIC_EHIP;
+    if (st == GIC_OK) memcpy(out, b.h_out, out_bytes);
     t_block_status = st;
     if (st != GIC_OK) {
         fprintf(stderr, "gfx_imagecompress_amd: block encode failed (%d)\n", st);
@@ -988,12 +1013,14 @@ extern "C" void Image_CompressRichGel999BC7enc16(uint32_t const input[16], bool 
     gic_default_options(&o);
     bc7enc_options(o, fast, perceptual);
     DeviceScratch &s = t_scratch;
-    const bool ok = s.reserve(64, 16) &&
-                    hipMemcpyAsync(s.src, input, 64, hipMemcpyHostToDevice, s.stream) == hipSuccess &&
-                    gic_hip_encode_blocks_u8(GIC_FMT_BC7ENC16, (const uint32_t *)s.src, 1, &o, (uint8_t *)s.dst,
-                                             s.stream) == GIC_OK &&
-                    hipMemcpyAsync(out, s.dst, 16, hipMemcpyDeviceToHost, s.stream) == hipSuccess &&
-                    hipStreamSynchronize(s.stream) == hipSuccess;
+    BlockStage &b = t_stage;
+    bool ok = s.reserve(0, 0) && b.ready();
+    if (ok) memcpy(b.h_in, input, 64);
+    ok = ok &&
+         gic_hip_encode_blocks_u8(GIC_FMT_BC7ENC16, (const uint32_t *)b.d_in, 1, &o, (uint8_t *)b.d_out, s.stream) ==
+             GIC_OK &&
+         hipStreamSynchronize(s.stream) == hipSuccess;
+    if (ok) memcpy(out, b.h_out, 16);
     t_block_status = ok ? GIC_OK : GIC_EHIP;
     if (!ok) {
         fprintf(stderr, "gfx_imagecompress_amd: block encode failed on the GPU\n");
