@@ -28,10 +28,14 @@ def t(fmt, src, ch, channel):
         gic.encode_device(fmt, src, n, n, 1, ch, dst, o)
     e.record()
     torch.cuda.synchronize()
+    import hashlib
+    t.dig = hashlib.sha1(dst.cpu().numpy().tobytes()).hexdigest()[:12]
     return s.elapsed_time(e) / reps
 
 
 for name, (src, ch) in srcs.items():
     for c in range(ch):
-        print(f"BC4 {name} channel {c}: {t(4, src, ch, c):.4f} ms", flush=True)
-print(f"BC5 normal RG8: {t(5, srcs['normal RG8'][0], 2, 0):.4f} ms", flush=True)
+        ms = t(4, src, ch, c)
+        print(f"{os.environ.get('GIC_LIBRARY', '')} BC4 {name} channel {c}: {ms:.4f} ms  digest {t.dig}", flush=True)
+ms = t(5, srcs['normal RG8'][0], 2, 0)
+print(f"{os.environ.get('GIC_LIBRARY', '')} BC5 normal RG8: {ms:.4f} ms  digest {t.dig}", flush=True)
