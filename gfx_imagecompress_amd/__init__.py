@@ -154,6 +154,8 @@ def library() -> ctypes.CDLL:
     lib.gic_hip_encode_blocks_u8.restype = ctypes.c_int
     lib.gic_hip_decode.argtypes = [ctypes.c_int, vp, u32, u32, u32, vp, sz, vp]
     lib.gic_hip_decode.restype = ctypes.c_int
+    lib.gic_hip_decode_bc6h.argtypes = [ctypes.c_int, vp, u32, u32, u32, vp, sz, vp]
+    lib.gic_hip_decode_bc6h.restype = ctypes.c_int
     lib.gic_decompress_image.argtypes = [vp]
     lib.gic_decompress_image.restype = vp
     lib.gic_save_dds.argtypes = [vp, ctypes.c_char_p]
@@ -341,6 +343,23 @@ def decode_device(fmt: int, blocks, width: int, height: int, slices: int, out, r
         raise GicError("out tensor too small for the given shape")
     _check(library().gic_hip_decode(fmt, blocks.data_ptr(), width, height, slices, out.data_ptr(), pitch,
                                     _stream_handle(stream)))
+
+
+def decode_bc6h_device(fmt: int, blocks, width: int, height: int, slices: int, out, row_pitch: int | None = None,
+                       stream=None) -> None:
+    """Asynchronously decode BC6H blocks (uint8 CUDA tensor) into ``out`` (a CUDA
+    tensor of slices*height rows of row_pitch bytes, 4 half floats per texel,
+    alpha 1.0) -- gic_hip_decode_bc6h."""
+    if not (blocks.is_cuda and out.is_cuda):
+        raise GicError("decode_bc6h_device needs device (HBM) tensors; there is no CPU path")
+    bx, by = blocks_shape(width, height)
+    if blocks.numel() * blocks.element_size() < bx * by * slices * 16:
+        raise GicError("blocks tensor too small for the given shape")
+    pitch = width * 8 if row_pitch is None else row_pitch
+    if not out.is_contiguous() or out.numel() * out.element_size() < pitch * height * slices:
+        raise GicError("out tensor too small for the given shape")
+    _check(library().gic_hip_decode_bc6h(fmt, blocks.data_ptr(), width, height, slices, out.data_ptr(), pitch,
+                                         _stream_handle(stream)))
 
 
 def _host_compress(fmt: int, image, options: Options):

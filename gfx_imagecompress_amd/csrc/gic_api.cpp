@@ -46,6 +46,8 @@ hipError_t launch_bc7enc_image(const Geometry &g, const gic_options &o, void *ds
 hipError_t launch_bc7enc_blocks_u8(const uint32_t *blocks, uint32_t n, const gic_options &o, void *dst, hipStream_t s);
 hipError_t launch_bc7enc_blocks_f32(const float *blocks, uint32_t n, const gic_options &o, void *dst, hipStream_t s);
 hipError_t launch_bc6h_blocks(const float *blocks, uint32_t n, int is_signed, void *dst, double *err, hipStream_t s);
+hipError_t launch_bc6h_decode(const uint8_t *blocks, uint32_t width, uint32_t height, uint32_t slices, int is_signed,
+                              uint16_t *out, size_t row_pitch, hipStream_t s);
 hipError_t launch_bc6h_image(const Geometry &g, int is_signed, int force_alpha_one, void *dst, double *err,
                              hipStream_t s);
 hipError_t bc7_iter_cap(int cap, unsigned long long *hits, int reset);
@@ -356,6 +358,17 @@ extern "C" int gic_hip_decode(gic_format fmt, const uint8_t *d_blocks, uint32_t 
                              ? gic::launch_bc7_decode(d_blocks, width, height, slices, d_rgba, row_pitch, (hipStream_t)stream)
                              : gic::launch_bcx_decode(d_blocks, (int)fmt, width, height, slices, d_rgba, row_pitch,
                                                       (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e);
+    return GIC_OK;
+}
+
+extern "C" int gic_hip_decode_bc6h(gic_format fmt, const uint8_t *d_blocks, uint32_t width, uint32_t height,
+                                   uint32_t slices, uint16_t *d_rgba16f, size_t row_pitch, void *stream)
+{
+    if (!is_bc6h(fmt) || !d_blocks || !d_rgba16f || !width || !height || !slices) return GIC_EINVAL;
+    if (row_pitch < (size_t)width * 8 || (row_pitch & 1)) return GIC_EINVAL;
+    const hipError_t e = gic::launch_bc6h_decode(d_blocks, width, height, slices, fmt == GIC_FMT_BC6H_SF, d_rgba16f,
+                                                 row_pitch, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e);
     return GIC_OK;
 }

@@ -29,6 +29,7 @@
 
 #include "gic_common.h"
 #include "bc7_tables.h"
+#include "bc6h_layout.h"
 
 namespace gic {
 namespace bc6h {
@@ -535,15 +536,21 @@ __device__ void shake_hd_wave(const float x[3], int idxt, uint32_t mask, ShakeOu
     const float y0 = rbf(x[0], f0), y1 = rbf(x[1], f0), y2 = rbf(x[2], f0);
     const bool alls = __all(!mem || (x[0] == y0 && x[1] == y1 && x[2] == y2));
     // index_collapse_kernel (:1688-1713)
-    int mi = 0x7fffffff, Mx = -0x7fffffff;
-    for (uint32_t mm = mask; mm; mm &= mm - 1) {
-        const int v = rbi(idxt, __builtin_ctz(mm));
-        mi = mi < v ? mi : v;
-        Mx = Mx > v ? Mx : v;
-    }
-    int D = 1;
-    for (int d = 2; d <= Mx - mi; d++)
-        if (__all(!mem || (idxt - mi) % d == 0)) D = d;
+    // the set W of the members' indices (< 16): its lowest bit is the minimum
+    // and its highest the maximum
+    unsigned W = 0;
+    for (uint32_t mm = mask; mm; mm &= mm - 1) W |= 1u << (rbi(idxt, __builtin_ctz(mm)) & 15);
+    const int mi = __builtin_ctz(W), Mx = 31 - __builtin_clz(W);
+    // D = the largest d <= Mx - mi dividing every member's offset idx - mi: the
+    // offsets form the 16-bit set V, and lane d tests V against the set of
+    // multiples of d -- one ballot instead of a loop of per-lane integer
+    // remainders (a ~20-instruction emulated division each)
+    const unsigned V = W >> mi;
+    unsigned mult = 0;
+    if (L >= 2 && L < 16)
+        for (int x = 0; x < 16; x += L) mult |= 1u << x;
+    const unsigned long long ok = __ballot(L >= 2 && L <= Mx - mi && (V & ~mult) == 0u);
+    const int D = ok ? 63 - __builtin_clzll(ok) : 1;
     const int c0 = mem ? (idxt - mi) / D : 0;
     const int Mi = (Mx - mi) / D;
     float err_o = 3.402823466e+38f;
@@ -1350,6 +1357,130 @@ __global__ void __launch_bounds__(256) k_bc6h_encode(uint32_t first, uint32_t n,
     if (err_out) err_out[first + b] = (double)error;
 }
 
+// --------------------------------------------------------------- decoder ---
+//
+// gic_hip_decode_bc6h: BC6H blocks back to RGBA16F texels (alpha 1.0), one lane
+// per block, from the format description -- the header layouts of
+// bc6h_layout.h (tools/gen_bc6h_layout.py, a transcription independent of the
+// encoder's kLayout), endpoint sign extension and inverse transform,
+// unquantisation, the 3/4-bit weights and the 31/64 (unsigned) or 31/32
+// (signed) finish.  Reserved modes decode to zero.
+
+__constant__ int kWeights3[8] = {0, 9, 18, 27, 37, 46, 55, 64};
+__constant__ int kWeights4[16] = {0, 4, 9, 13, 17, 21, 26, 30, 34, 38, 43, 47, 51, 55, 60, 64};
+
+__device__ __forceinline__ int dec_sext(int x, int bits) { return (x << (32 - bits)) >> (32 - bits); }
+
+__device__ __forceinline__ int dec_unq(int x, int bits, bool is_signed)
+{
+    if (!is_signed) {
+        if (bits >= 15) return x;
+        if (x == 0) return 0;
+        if (x == (1 << bits) - 1) return 0xFFFF;
+        return ((x << 16) + 0x8000) >> bits;
+    }
+    if (bits >= 16) return x;
+    const bool neg = x < 0;
+    const int a = neg ? -x : x;
+    int u;
+    if (a == 0)
+        u = 0;
+    else if (a >= (1 << (bits - 1)) - 1)
+        u = 0x7FFF;
+    else
+        u = ((a << 15) + 0x4000) >> (bits - 1);
+    return neg ? -u : u;
+}
+
+__device__ __forceinline__ uint32_t dec_finish(int v, bool is_signed)
+{
+    if (!is_signed) return (uint32_t)((v * 31) >> 6);
+    const int h = v < 0 ? -(((-v) * 31) >> 5) : (v * 31) >> 5;
+    return h < 0 ? (0x8000u | (uint32_t)(-h)) : (uint32_t)h;
+}
+
+__global__ void __launch_bounds__(256) k_bc6h_decode(const uint8_t *__restrict__ blocks, uint32_t width, uint32_t height,
+                                                     uint32_t slices, int is_signed, uint16_t *__restrict__ out,
+                                                     size_t row_pitch)
+{
+    const uint32_t bx = (width + 3) / 4, by = (height + 3) / 4;
+    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= bx * by * slices) return;
+    const uint32_t sl = id / (bx * by), r = id % (bx * by), y0 = (r / bx) * 4, x0 = (r % bx) * 4;
+    const uint4 w = reinterpret_cast<const uint4 *>(blocks)[id];
+    const uint64_t lo = (uint64_t)w.x | ((uint64_t)w.y << 32), hi = (uint64_t)w.z | ((uint64_t)w.w << 32);
+    auto bit = [&](uint32_t p) -> uint32_t { return (uint32_t)((p < 64 ? lo >> p : hi >> (p - 64)) & 1u); };
+    auto take = [&](uint32_t &p, uint32_t n) -> uint32_t {
+        uint32_t v = 0;
+        for (uint32_t k = 0; k < n; ++k) v |= bit(p + k) << k;
+        p += n;
+        return v;
+    };
+    int mode = -1;
+    const uint32_t m2 = w.x & 3u, m5 = w.x & 31u;
+    for (int m = 0; m < 14; ++m) {
+        const ModeDesc &d = kDecModes[m];
+        if ((d.mode_bits == 2 && m2 == d.value) || (d.mode_bits == 5 && m2 >= 2 && m5 == d.value)) {
+            mode = m;
+            break;
+        }
+    }
+    uint16_t tex[16][3];
+    if (mode < 0) {
+        for (int t = 0; t < 16; ++t) tex[t][0] = tex[t][1] = tex[t][2] = 0;
+    } else {
+        const ModeDesc d = kDecModes[mode];
+        uint32_t p = d.mode_bits;
+        int f[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int e = 0; e < d.n; ++e) {
+            const int code = kDecLayout[mode][e];
+            f[code >> 4] |= (int)take(p, 1) << (code & 15);
+        }
+        const int regions = d.regions, nends = 2 * regions;
+        const uint32_t part = regions == 2 ? take(p, 5) : 0u;
+        const int epb = d.ep_bits;
+        int ep[4][3];
+        for (int e = 0; e < 4; ++e)
+            for (int c = 0; c < 3; ++c) ep[e][c] = f[e * 3 + c];
+        for (int c = 0; c < 3; ++c) {
+            if (is_signed) ep[0][c] = dec_sext(ep[0][c], epb);
+            for (int e = 1; e < nends; ++e) {
+                if (d.transformed) {
+                    const int v = (ep[0][c] + dec_sext(ep[e][c], d.delta_bits[c])) & ((1 << epb) - 1);
+                    ep[e][c] = is_signed ? dec_sext(v, epb) : v;
+                } else if (is_signed) {
+                    ep[e][c] = dec_sext(ep[e][c], epb);
+                }
+            }
+        }
+        int unq[4][3];
+        for (int e = 0; e < nends; ++e)
+            for (int c = 0; c < 3; ++c) unq[e][c] = dec_unq(ep[e][c], epb, is_signed != 0);
+        const uint32_t shape = regions == 2 ? dShape[part] : 0u;
+        const uint32_t anc = regions == 2 ? dAnchor[part] : 0u;
+        const uint32_t ib = regions == 2 ? 3 : 4;
+        for (int t = 0; t < 16; ++t) {
+            const bool anchor = t == 0 || (regions == 2 && (uint32_t)t == anc);
+            const uint32_t idx = take(p, anchor ? ib - 1 : ib);
+            const int wgt = ib == 3 ? kWeights3[idx] : kWeights4[idx];
+            const int rg = (int)((shape >> (2 * t)) & 3u);
+            for (int c = 0; c < 3; ++c) {
+                const int v = ((64 - wgt) * unq[2 * rg][c] + wgt * unq[2 * rg + 1][c] + 32) >> 6;
+                tex[t][c] = (uint16_t)dec_finish(v, is_signed != 0);
+            }
+        }
+    }
+    for (int t = 0; t < 16; ++t) {
+        const uint32_t x = x0 + (t & 3), y = y0 + (t >> 2);
+        if (x >= width || y >= height) continue;
+        uint16_t *o = (uint16_t *)((uint8_t *)out + ((size_t)sl * height + y) * row_pitch) + (size_t)x * 4;
+        o[0] = tex[t][0];
+        o[1] = tex[t][1];
+        o[2] = tex[t][2];
+        o[3] = 0x3C00;   // 1.0
+    }
+}
+
 // ------------------------------------------------------------------ host ---
 
 constexpr uint32_t kChunk = 1u << 16;
@@ -1438,6 +1569,21 @@ hipError_t bc6h_iter_cap(int cap, unsigned long long *hits, int reset)
     }
     if (e == hipSuccess && cap >= 0) e = hipMemcpyToSymbol(HIP_SYMBOL(bc6h::g_iter_cap), &cap, sizeof(cap));
     return e;
+}
+
+hipError_t launch_bc6h_decode(const uint8_t *blocks, uint32_t width, uint32_t height, uint32_t slices, int is_signed,
+                              uint16_t *out, size_t row_pitch, hipStream_t s)
+{
+    using namespace bc6h;
+    {
+        std::lock_guard<std::mutex> lk(g_bc6h_lock);
+        const hipError_t e = upload_tables();
+        if (e != hipSuccess) return e;
+    }
+    const uint64_t n = (uint64_t)((width + 3) / 4) * ((height + 3) / 4) * slices;
+    hipLaunchKernelGGL(k_bc6h_decode, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, blocks, width, height, slices,
+                       is_signed, out, row_pitch);
+    return hipGetLastError();
 }
 
 hipError_t launch_bc6h_blocks(const float *blocks, uint32_t n, int is_signed, void *dst, double *err, hipStream_t s)

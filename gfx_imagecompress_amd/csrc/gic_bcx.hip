@@ -1505,9 +1505,11 @@ __global__ void __launch_bounds__(256, 2) bc23_image_kernel(Geometry g, int fmt,
 // texels as packed bytes (row loads of 4 / 8 / 16 bytes for 1 / 2 / 4
 // channels), each selected byte to v / 255.0f through a 256-entry LDS table.
 // (A float RGBA gather indexed by a runtime channel went to scratch: 608 bytes
-// per lane.)
+// per lane.)  Budgeted for 6 waves/SIMD (BC4, 80 VGPRs, one spilled) and 5
+// (BC5, 96, four spilled): 8K BC4 0.261 -> 0.255 ms, BC5 0.924 -> 0.859 ms against
+// the unconstrained 81 / 97-VGPR build, same blocks (profiles/r04f_bc45_ab.txt).
 template <int FMT>
-__global__ void __launch_bounds__(256) bc45_image_kernel(Geometry g, int channel, uint64_t *__restrict__ dst)
+__global__ void __launch_bounds__(256, FMT == 4 ? 6 : 5) bc45_image_kernel(Geometry g, int channel, uint64_t *__restrict__ dst)
 {
     __shared__ float lut[256];   // byte -> v / 255.0f
     __shared__ float wk_uv[16 * 256];     // CompBlock1's uv of each lane

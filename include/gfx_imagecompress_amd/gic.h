@@ -156,6 +156,13 @@ int gic_hip_encode_blocks_u8(gic_format fmt, const uint32_t *d_blocks, uint32_t 
 int gic_hip_decode(gic_format fmt, const uint8_t *d_blocks, uint32_t width, uint32_t height, uint32_t slices,
                    uint8_t *d_rgba, size_t row_pitch, void *stream);
 
+/* BC6H (GIC_FMT_BC6H / GIC_FMT_BC6H_SF) blocks to RGBA16F texels on the device:
+ * 4 half-float bit patterns per texel (alpha 1.0), row_pitch >= width * 8 bytes,
+ * decoded from the BC6H format description (not from the encoder's tables);
+ * reserved modes decode to zero.  An extension: the reference has no decoder. */
+int gic_hip_decode_bc6h(gic_format fmt, const uint8_t *d_blocks, uint32_t width, uint32_t height, uint32_t slices,
+                        uint16_t *d_rgba16f, size_t row_pitch, void *stream);
+
 /* Host image helpers (extensions; the reference has neither):
  *   gic_decompress_image: a BC1/BC2/BC3/BC4/BC5/BC7 image (as the
  *     Image_CompressAMD* functions return) decoded on the GPU to an RGBA8

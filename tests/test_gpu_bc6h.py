@@ -187,3 +187,52 @@ def test_bc6h_gpu_blocks_decode_independently(gpu):
         assert 1 <= d["mode"] <= 10, (k, d["mode"])
         dec = np.abs(_input_half_int(blocks[k], False) - _half_int(d["texels"].view(np.float16))).sum()
         assert abs(dec - gerr[k]) <= 48, (k, d["mode"], dec, gerr[k])
+
+
+@pytest.mark.parametrize("signed", [False, True])
+def test_bc6h_device_decoder_matches_the_test_decoder(gpu, signed):
+    """gic_hip_decode_bc6h (the product's decoder, its own transcription of the
+    format's layouts) gives the same half texels as tests/bc6h_decode.py on the
+    kernels' blocks of a ragged HDR image, every mode the encoder reaches."""
+    import torch
+    import bc6h_decode as D
+    w, h = 70, 38
+    img = synth.hdr_rgba(w, h, seed=9, signed=signed)
+    src = torch.from_numpy(img.reshape(-1).copy()).cuda()
+    bx, by = (w + 3) // 4, (h + 3) // 4
+    fmt = gic.FMT_BC6H_SF if signed else gic.FMT_BC6H
+    dst = torch.zeros(bx * by * 16, dtype=torch.uint8, device="cuda")
+    gic.encode_device_src(fmt, gic.SRC_FLOAT32, src, w, h, 1, 4, dst)
+    out = torch.zeros(h * w * 4, dtype=torch.int16, device="cuda")
+    gic.decode_bc6h_device(fmt, dst, w, h, 1, out)
+    torch.cuda.synchronize()
+    blocks = dst.cpu().numpy().reshape(by, bx, 16)
+    got = out.cpu().numpy().view(np.uint16).reshape(h, w, 4)
+    assert (got[:, :, 3] == 0x3C00).all()
+    for y in range(by):
+        for x in range(bx):
+            d = D.decode_block(blocks[y, x], signed)
+            want = d["texels"].reshape(4, 4, 3)
+            ys, xs = min(4, h - 4 * y), min(4, w - 4 * x)
+            assert np.array_equal(got[4 * y:4 * y + ys, 4 * x:4 * x + xs, :3], want[:ys, :xs]), (y, x, d["mode"])
+
+
+def test_bc6h_full_image_round_trip(gpu):
+    """Full-size property check: a 1024^2 HDR ramp encoded and decoded on the GPU
+    reproduces its input within 2 % relative L1 per block (half-float integer
+    space), the bound tests/test_bc6h_decode.py pins on the restatement."""
+    import torch
+    n = 1024
+    img = synth.hdr_rgba(n, n, seed=1)
+    src = torch.from_numpy(img.reshape(-1).copy()).cuda()
+    dst = torch.zeros((n // 4) ** 2 * 16, dtype=torch.uint8, device="cuda")
+    gic.encode_device_src(gic.FMT_BC6H, gic.SRC_FLOAT32, src, n, n, 1, 4, dst)
+    out = torch.zeros(n * n * 4, dtype=torch.int16, device="cuda")
+    gic.decode_bc6h_device(gic.FMT_BC6H, dst, n, n, 1, out)
+    torch.cuda.synchronize()
+    dec = out.cpu().numpy().view(np.uint16).reshape(n, n, 4)[:, :, :3].astype(np.int64)
+    want = np.where(img[:, :, :3] < 0.00001, 0, img[:, :, :3].astype(np.float16).view(np.uint16)).astype(np.int64)
+    d = np.abs(dec - want).reshape(n // 4, 4, n // 4, 4, 3).sum(axis=(1, 3, 4))
+    m = want.reshape(n // 4, 4, n // 4, 4, 3).sum(axis=(1, 3, 4))
+    rel = d / np.maximum(m, 1)
+    assert rel.max() <= 0.02, float(rel.max())
