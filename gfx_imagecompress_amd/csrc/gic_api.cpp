@@ -918,8 +918,10 @@ struct BlockStage {
     bool ready()
     {
         if (d_in && d_out) return true;
-        if (!h_in && hipHostMalloc((void **)&h_in, 64 * sizeof(float), hipHostMallocMapped) != hipSuccess) return false;
-        if (!h_out && hipHostMalloc((void **)&h_out, 64, hipHostMallocMapped) != hipSuccess) return false;
+        // fine-grained (coherent): the GPU never caches a previous call's block
+        const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+        if (!h_in && hipHostMalloc((void **)&h_in, 64 * sizeof(float), fl) != hipSuccess) return false;
+        if (!h_out && hipHostMalloc((void **)&h_out, 64, fl) != hipSuccess) return false;
         return hipHostGetDevicePointer(&d_in, h_in, 0) == hipSuccess &&
                hipHostGetDevicePointer(&d_out, h_out, 0) == hipSuccess;
     }

@@ -70,6 +70,11 @@ def test_block_bytes_and_argument_checks():
     for bound in (float("nan"), -1.0, 70000.0):   # bc7_mse_bound: NaN, negative, above 255^2
         o = gic.Options(bc7_mse_bound=bound).to_c()
         assert lib.gic_hip_encode(gic.FMT_BC7, 16, 4, 4, 1, 4, 16, ctypes.byref(o), 16, None, None) == gic.GIC_EINVAL
+    # BC6H decoder: BC6H formats only, RGBA16F rows of at least width * 8 bytes
+    assert lib.gic_hip_decode_bc6h(gic.FMT_BC7, 16, 4, 4, 1, 16, 32, None) == gic.GIC_EINVAL
+    assert lib.gic_hip_decode_bc6h(gic.FMT_BC6H, 16, 4, 4, 1, 16, 31, None) == gic.GIC_EINVAL
+    assert lib.gic_hip_decode_bc6h(gic.FMT_BC6H, None, 4, 4, 1, 16, 32, None) == gic.GIC_EINVAL
+    assert lib.gic_hip_decode(gic.FMT_BC6H, 16, 4, 4, 1, 16, 16, None) == gic.GIC_EINVAL
 
 
 def test_image_model_and_pick_type():
