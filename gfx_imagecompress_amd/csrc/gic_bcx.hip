@@ -1071,12 +1071,34 @@ __device__ __forceinline__ uint2 encode_bc1_u8_lds(const uint32_t px[16], int st
     int kept;
     ColLT<S1> ul;
     {
-        ColB u;
-        u.lut = lut;
-        unique_colours(u, px, use_alpha, thr_keep, kept);
+        // unique_colours with each leader's word stored straight to its LDS
+        // row (row = its rank) instead of selected into 16 registers first
+        // (with the word parts formed at the store: 150 -> 120 VGPRs, 4
+        // waves/SIMD -- the LDS limit -- 8K G1 9.54 -> 9.17 ms, same blocks)
+        uint32_t key[16];
+        bool lead[16];
+        int ui[16], cnt[16];
+        kept = 0;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) lds_st_u(w + 4u * (uint32_t)(i * kLdsStride), u.u[i]);
-        ul.n = u.n;
+        for (int i = 0; i < 16; ++i) {
+            const bool live = !use_alpha || (px[i] >> 24) >= thr_keep;
+            key[i] = live ? ((px[i] & 0xffu) << 16) | (px[i] & 0xff00u) | ((px[i] >> 16) & 0xffu) : 0xffffffffu;
+            kept += live ? 1 : 0;
+        }
+        rank_keys(key, lead, ui, cnt);
+        int n = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) lds_st_u(w + 4u * (uint32_t)(i * kLdsStride), 0u);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            if (!lead[i]) continue;
+            uint32_t c = px[i];
+            asm volatile("" : "+v"(c));   // the word's parts formed here, not hoisted and held
+            const uint32_t word = ((c >> 16) & 0xffu) | (c & 0xff00u) | ((c & 0xffu) << 16) | ((uint32_t)cnt[i] << 24);
+            lds_st_u(w + 4u * (uint32_t)kLdsStride * (uint32_t)ui[i], word);
+            n++;
+        }
+        ul.n = n;
     }
     ul.w = w;
     ul.lut = lut;
