@@ -1064,42 +1064,47 @@ __device__ __forceinline__ uint2 encode_bc1_u8(const uint32_t px[16], int steps,
 }
 
 // the same with the colour words parked in LDS (ColL; w = this lane's column)
+// unique_colours with each leader's word stored straight to its LDS row (row
+// = its rank, w = this lane's column) instead of selected into 16 registers
+// first, the word parts formed at the store (the BC1 kernel: 150 -> 120
+// VGPRs, 4 waves/SIMD -- the LDS limit -- 8K G1 9.54 -> 9.17 ms, same blocks).
+// Returns the number of unique colours.
+__device__ __forceinline__ int unique_colours_lds(const uint32_t px[16], bool use_alpha, uint32_t thr_keep, uint32_t w,
+                                                  int &kept)
+{
+    uint32_t key[16];
+    bool lead[16];
+    int ui[16], cnt[16];
+    kept = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const bool live = !use_alpha || (px[i] >> 24) >= thr_keep;
+        key[i] = live ? ((px[i] & 0xffu) << 16) | (px[i] & 0xff00u) | ((px[i] >> 16) & 0xffu) : 0xffffffffu;
+        kept += live ? 1 : 0;
+    }
+    rank_keys(key, lead, ui, cnt);
+    int n = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) lds_st_u(w + 4u * (uint32_t)(i * kLdsStride), 0u);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (!lead[i]) continue;
+        uint32_t c = px[i];
+        asm volatile("" : "+v"(c));   // the word's parts formed here, not hoisted and held
+        const uint32_t word = ((c >> 16) & 0xffu) | (c & 0xff00u) | ((c & 0xffu) << 16) | ((uint32_t)cnt[i] << 24);
+        lds_st_u(w + 4u * (uint32_t)kLdsStride * (uint32_t)ui[i], word);
+        n++;
+    }
+    return n;
+}
+
 template <bool R3D, bool S1, class Tex>
 __device__ __forceinline__ uint2 encode_bc1_u8_lds(const uint32_t px[16], int steps, bool use_alpha, uint32_t thr_keep,
                                                    const Tex &t, uint32_t lut, uint32_t w)
 {
     int kept;
     ColLT<S1> ul;
-    {
-        // unique_colours with each leader's word stored straight to its LDS
-        // row (row = its rank) instead of selected into 16 registers first
-        // (with the word parts formed at the store: 150 -> 120 VGPRs, 4
-        // waves/SIMD -- the LDS limit -- 8K G1 9.54 -> 9.17 ms, same blocks)
-        uint32_t key[16];
-        bool lead[16];
-        int ui[16], cnt[16];
-        kept = 0;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const bool live = !use_alpha || (px[i] >> 24) >= thr_keep;
-            key[i] = live ? ((px[i] & 0xffu) << 16) | (px[i] & 0xff00u) | ((px[i] >> 16) & 0xffu) : 0xffffffffu;
-            kept += live ? 1 : 0;
-        }
-        rank_keys(key, lead, ui, cnt);
-        int n = 0;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) lds_st_u(w + 4u * (uint32_t)(i * kLdsStride), 0u);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            if (!lead[i]) continue;
-            uint32_t c = px[i];
-            asm volatile("" : "+v"(c));   // the word's parts formed here, not hoisted and held
-            const uint32_t word = ((c >> 16) & 0xffu) | (c & 0xff00u) | ((c & 0xffu) << 16) | ((uint32_t)cnt[i] << 24);
-            lds_st_u(w + 4u * (uint32_t)kLdsStride * (uint32_t)ui[i], word);
-            n++;
-        }
-        ul.n = n;
-    }
+    ul.n = unique_colours_lds(px, use_alpha, thr_keep, w, kept);
     ul.w = w;
     ul.lut = lut;
     return encode_bc1<R3D>(ul, kept, t, steps, use_alpha);
@@ -1199,7 +1204,10 @@ struct LdsArr {
     __device__ __forceinline__ float &operator[](int k) const { return p[k * 256]; }
 };
 // repeat counts (1..16) as bytes: a lane's 16 uv floats + 16 ur bytes = 80 B of LDS
-struct LdsCount {
+// (STRIDE: bytes between a lane's counts; 1024 puts count k in byte 0 of the
+// lane's own word k of a 256-lane word array)
+template <int STRIDE = 256>
+struct LdsCountT {
     uint8_t *p;
     struct Ref {
         uint8_t *q;
@@ -1207,14 +1215,19 @@ struct LdsCount {
         __device__ __forceinline__ Ref &operator=(float x) { *q = (uint8_t)x; return *this; }
         __device__ __forceinline__ Ref &operator+=(float x) { *q = (uint8_t)((float)*q + x); return *this; }
     };
-    __device__ __forceinline__ Ref operator[](int k) const { return Ref{p + k * 256}; }
+    __device__ __forceinline__ Ref operator[](int k) const { return Ref{p + k * STRIDE}; }
 };
+using LdsCount = LdsCountT<256>;
 struct Bc4Scratch {
     PrivArr uv, ur;
 };
 struct Bc4Lds {
     LdsArr uv;
     LdsCount ur;
+};
+struct Bc4LdsW {   // counts in the lanes' own words (the BC3 kernel borrows its texel array)
+    LdsArr uv;
+    LdsCountT<1024> ur;
 };
 
 // RmpSrch1 evaluated in full, amd_bcx_body.cpp:1510-1548
@@ -1492,10 +1505,12 @@ __global__ void __launch_bounds__(256, 3) bc1_image_kernel(Geometry g, Bc1Params
 // Image_CompressAMDAlphaSingleModeBlock) then the 4-colour RGB half, one lane
 // per block.  Alpha is the source's (1.0 without an alpha channel, as
 // ReadNxNSplitBlockF's forceAlphaTo1).
-template <bool R3D>
+template <bool R3D, bool S1>
 __global__ void __launch_bounds__(256, 2) bc23_image_kernel(Geometry g, int fmt, Bc1Params p, uint4 *__restrict__ dst)
 {
     __shared__ float lut[256];   // byte -> v / 255.0f
+    __shared__ uint32_t cols[16 * bcx::kLdsStride];   // the colour half's unique colours (ColL)
+    __shared__ uint32_t texs[16 * bcx::kLdsStride];   // and the block's texels (TexL), as the BC1 kernel
     lut[threadIdx.x] = (float)threadIdx.x / 255.0f;
     __syncthreads();
     const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1506,20 +1521,29 @@ __global__ void __launch_bounds__(256, 2) bc23_image_kernel(Geometry g, int fmt,
     load_block_u8(g, slice, by, bx, p.force_alpha_one != 0, px);
     uint2 a;
     if (fmt == 3) {
+        // BC3's alpha half runs first: CompBlock1's running arrays borrow this
+        // lane's columns of cols (uv) and texs (repeat counts) -- as the BC4
+        // kernel, instead of 132 B of scratch per lane
+        const bcx::Bc4LdsW wk{{reinterpret_cast<float *>(cols) + threadIdx.x},
+                              {reinterpret_cast<uint8_t *>(texs + threadIdx.x)}};
         float v[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) v[i] = lut[px[i] >> 24];
-        const uint64_t r = bcx::encode_bc4(v);
+        const uint64_t r = bcx::encode_bc4(v, wk);
         a = make_uint2((uint32_t)r, (uint32_t)(r >> 32));
     } else {
         a = bcx::encode_explicit_alpha_u8(px);
     }
-    bcx::ColB u;
-    u.lut = bcx::lds_off(lut);
+    const uint32_t ta = bcx::lds_off(texs + threadIdx.x);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) bcx::lds_st_u(ta + 4u * (uint32_t)(i * bcx::kLdsStride), px[i]);
+    const bcx::TexL t{ta, 0u};
+    bcx::ColLT<S1> ul;
     int kept;
-    bcx::unique_colours(u, px, false, 0u, kept);
-    const bcx::TexB t{px, 0u};
-    const uint2 c = bcx::encode_rgb4<R3D>(u, kept, t, p.steps);
+    ul.w = bcx::lds_off(cols + threadIdx.x);
+    ul.n = bcx::unique_colours_lds(px, false, 0u, ul.w, kept);
+    ul.lut = bcx::lds_off(lut);
+    const uint2 c = bcx::encode_rgb4<R3D>(ul, kept, t, p.steps);
     dst[id] = make_uint4(a.x, a.y, c.x, c.y);
 }
 
@@ -1864,9 +1888,11 @@ hipError_t launch_bc23_image(const Geometry &g, int fmt, int steps, int force_al
     const Bc1Params p{0.f, steps, force_alpha_one, 0u, 0u};
     const uint32_t wg = 256, grid = (g.total + wg - 1) / wg;
     if (r3d)
-        hipLaunchKernelGGL(bc23_image_kernel<true>, dim3(grid), dim3(wg), 0, s, g, fmt, p, (uint4 *)dst);
+        hipLaunchKernelGGL((bc23_image_kernel<true, false>), dim3(grid), dim3(wg), 0, s, g, fmt, p, (uint4 *)dst);
+    else if (steps == 1)
+        hipLaunchKernelGGL((bc23_image_kernel<false, true>), dim3(grid), dim3(wg), 0, s, g, fmt, p, (uint4 *)dst);
     else
-        hipLaunchKernelGGL(bc23_image_kernel<false>, dim3(grid), dim3(wg), 0, s, g, fmt, p, (uint4 *)dst);
+        hipLaunchKernelGGL((bc23_image_kernel<false, false>), dim3(grid), dim3(wg), 0, s, g, fmt, p, (uint4 *)dst);
     return hipGetLastError();
 }
 
