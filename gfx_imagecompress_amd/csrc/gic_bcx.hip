@@ -1416,11 +1416,9 @@ __device__ float scalar_block(const float v[16], const float sorted[16], uint8_t
 
 // Image_CompressAMDAlphaSingleModeBlock + EncodeAlphaBlock,
 // amd_bcx_helpers.cpp:32-46, :125-140
-template <class W = Bc4Scratch>
-__device__ uint64_t encode_bc4(const float v[16], W wk = W())
+// ascending sort by rank (equal values are interchangeable)
+__device__ __forceinline__ void bc4_sort(const float v[16], float s[16])
 {
-    // ascending sort by rank (equal values are interchangeable)
-    float s[16];
     bool nan = false;
 #pragma unroll
     for (int i = 0; i < 16; ++i) nan = nan || v[i] != v[i];
@@ -1457,11 +1455,186 @@ __device__ uint64_t encode_bc4(const float v[16], W wk = W())
             s[0] = go ? t : s[0];
         }
     }
+}
+
+template <class W = Bc4Scratch>
+__device__ uint64_t encode_bc4(const float v[16], W wk = W())
+{
+    float s[16];
+    bc4_sort(v, s);
     uint8_t ep8[2], ep6[2];
     uint64_t i8, i6 = 0;
     const float e8 = scalar_block<8, false>(v, s, ep8, i8, wk);
     float e6 = 3.402823466e+38f;
     if (!(e8 == 0.f)) e6 = scalar_block<6, true>(v, s, ep6, i6, wk);
+    const bool use8 = e8 <= e6;
+    const uint8_t *ep = use8 ? ep8 : ep6;
+    return (uint64_t)ep[0] | ((uint64_t)ep[1] << 8) | ((use8 ? i8 : i6) << 16);
+}
+
+// ---- one 64-lane wave per block (small batches: the block-level entry points)
+//
+// A lane-per-block BC4 search on one noisy block is ~450 us of serial work on
+// one lane (RmpSrch1's grid of up to 12 x 12 ramps, then Refine1's hill climb of
+// 9 ramps a step).  Here every lane of the wave holds the block; the grid's
+// (sl, sr) pairs and each climb step's 9 candidates are spread over the lanes and
+// the sequential choice -- the first strictly smaller error in loop order -- is
+// recovered by a (error, order) minimum.  Every ramp error is the same function
+// of the same floats as in scalar_endpoints, so the blocks are bit-identical.
+
+// (e, order) of the lane with the smallest e, ties to the smallest order; a lane
+// without a candidate brings e = +inf
+__device__ __forceinline__ void wave_argmin(float &e, int &o)
+{
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        const float e2 = __shfl_xor(e, m);
+        const int o2 = __shfl_xor(o, m);
+        if (e2 < e || (e2 == e && o2 < o)) {
+            e = e2;
+            o = o2;
+        }
+    }
+}
+
+template <int N, bool FIXED>
+__device__ void scalar_endpoints_wave(float ramp[2], const float vals_sorted[16], float *uv, float *ur)
+{
+    // compaction: uniform, every lane writes the same values (uv / ur in LDS)
+    int nu = 0;
+    float prev = -2.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const float x = vals_sorted[i];
+        if (FIXED) {
+            if (prev != x) {
+                prev = x;
+                if (!((double)prev <= 1.5 / 255.) && !((double)prev >= 253.5 / 255.)) {
+                    uv[nu] = x;
+                    ur[nu] = 1.f;
+                    nu++;
+                }
+            } else if (nu > 0 && uv[nu - 1] == prev) {
+                ur[nu - 1] += 1.f;
+            }
+        } else {
+            if (prev != x) {
+                uv[nu] = prev = x;
+                ur[nu] = 1.f;
+                nu++;
+            } else {
+                ur[nu - 1] += 1.f;
+            }
+        }
+    }
+    if (nu <= 2) {
+        if (FIXED && nu == 0) {
+            ramp[0] = 128.f;
+            ramp[1] = ramp[0] + 1.f;
+        } else {
+            ramp[0] = floorf(uv[0] * 255.f + 0.5f);
+            ramp[1] = (nu == 1) ? ramp[0] + 1.f : floorf(uv[1] * 255.f + 0.5f);
+        }
+    } else {
+        const int ln = (int)(threadIdx.x & 63u);
+        float lo = uv[0], hi = uv[nu - 1];
+        float lr = lo, hr = hi;
+        const float cntr = (lr + hr) / 2;
+        float gerr = 128000.f;
+        if (!(hi - lo <= 48.f / 256.f)) {
+            const float llb = (0.f > lr - 0.1f) ? 0.f : lr - 0.1f;
+            const float rrb = (1.f < hr + 0.1f) ? 1.f : hr + 0.1f;
+            const float lrb = (cntr < lr + 0.1f) ? cntr : lr + 0.1f;
+            const float rlb = (cntr > hr - 0.1f) ? cntr : hr - 0.1f;
+            // the loops' own iteration counts (the same float steps)
+            int nl = 0, nr = 0;
+            for (float sl = llb; sl < lrb; sl += 0.018f) ++nl;
+            for (float sr = rrb; rlb <= sr; sr -= 0.018f) ++nr;
+            float be = __builtin_huge_valf();
+            int bo = 0x7fffffff;
+            for (int t = ln; t < nl * nr; t += 64) {
+                const int i = t / nr, j = t - i * nr;
+                float sl = llb, sr = rrb;
+                for (int k = 0; k < i; ++k) sl += 0.018f;
+                for (int k = 0; k < j; ++k) sr -= 0.018f;
+                const float e = scalar_ramp_error<N>(uv, ur, sl, sr, nu);
+                if (e < 128000.f && e < be) {   // first strictly smaller, per lane in loop order
+                    be = e;
+                    bo = t;
+                }
+            }
+            wave_argmin(be, bo);
+            float gl = 0.f, gr = 0.f;
+            if (bo != 0x7fffffff) {
+                const int i = bo / nr, j = bo - i * nr;
+                gl = llb;
+                gr = rrb;
+                for (int k = 0; k < i; ++k) gl += 0.018f;
+                for (int k = 0; k < j; ++k) gr -= 0.018f;
+                gerr = be;
+            }
+            lr = gl;
+            hr = gr;
+        }
+        // Refine1 hill climb, amd_bcx_body.cpp:1555-1607: lane m < 9 tries move m
+        const float mstep = 0.6f / 256.f;
+        // (mv = {0, -1, 1}: ca moves by mv[m / 3], cb by mv[m % 3])
+        const int ma = ln / 3, mb = ln % 3;
+        const float mva = ma == 0 ? 0.f : (ma == 1 ? -1.f : 1.f);
+        const float mvb = mb == 0 ? 0.f : (mb == 1 ? -1.f : 1.f);
+        for (;;) {
+            float ca = lr + mstep * mva;
+            float cb = hr + mstep * mvb;
+            ca = maxr(ca, 0.f);
+            cb = minr(cb, 1.f);
+            float e = __builtin_huge_valf();
+            int o = 0x7fffffff;
+            if (ln < 9) {
+                const float t = scalar_ramp_error<N>(uv, ur, ca, cb, nu);
+                if (t < gerr) {
+                    e = t;
+                    o = ln;
+                }
+            }
+            wave_argmin(e, o);
+            if (o == 0x7fffffff) break;
+            lr = __shfl(ca, o);
+            hr = __shfl(cb, o);
+            gerr = e;
+        }
+        lo = lr * 255.f;
+        hi = hr * 255.f;
+        ramp[1] = floorf(hi + 0.5f);
+        ramp[0] = floorf(lo + 0.5f);
+    }
+    if (ramp[0] == ramp[1]) {
+        if (ramp[1] < 255.f)
+            ramp[1]++;
+        else
+            ramp[1]--;
+    }
+}
+
+// encode_bc4 with the endpoint searches spread over the wave; every lane holds
+// v[] and returns the block.  uv / ur: 16 floats of LDS each, the wave's own.
+__device__ uint64_t encode_bc4_wave(const float v[16], float *uv, float *ur)
+{
+    float s[16];
+    bc4_sort(v, s);
+    uint8_t ep8[2], ep6[2];
+    uint64_t i8, i6 = 0;
+    float ramp[2];
+    scalar_endpoints_wave<8, false>(ramp, s, uv, ur);
+    const float e8 = scalar_cluster<8, false>(v, ramp, i8);
+    ep8[0] = (uint8_t)ramp[0];
+    ep8[1] = (uint8_t)ramp[1];
+    float e6 = 3.402823466e+38f;
+    if (!(e8 == 0.f)) {
+        scalar_endpoints_wave<6, true>(ramp, s, uv, ur);
+        e6 = scalar_cluster<6, true>(v, ramp, i6);
+        ep6[0] = (uint8_t)ramp[0];
+        ep6[1] = (uint8_t)ramp[1];
+    }
     const bool use8 = e8 <= e6;
     const uint8_t *ep = use8 ? ep8 : ep6;
     return (uint64_t)ep[0] | ((uint64_t)ep[1] << 8) | ((use8 ? i8 : i6) << 16);
@@ -1608,6 +1781,20 @@ __global__ void __launch_bounds__(256) bc4_blocks_kernel(const float *__restrict
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = blocks[(size_t)id * 16 + i];
     dst[id] = bcx::encode_bc4(v);
+}
+
+// one 64-lane workgroup (one wave) per block: small batches
+__global__ void __launch_bounds__(64) bc4_blocks_wave_kernel(const float *__restrict__ blocks, uint32_t n,
+                                                             uint64_t *__restrict__ dst)
+{
+    __shared__ float uv[16], ur[16];
+    const uint32_t id = blockIdx.x;
+    if (id >= n) return;
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = blocks[(size_t)id * 16 + i];
+    const uint64_t b = bcx::encode_bc4_wave(v, uv, ur);
+    if (threadIdx.x == 0) dst[id] = b;
 }
 
 template <bool R3D>
@@ -1928,8 +2115,17 @@ hipError_t launch_bc1_blocks(const float *blocks, uint32_t n, float thr, int ste
     return hipGetLastError();
 }
 
+// Below this many blocks a wave per block (bc4_blocks_wave_kernel) finishes
+// sooner than a lane per block: the batch cannot fill the chip lane-wise, and a
+// block's serial search is the call's latency.
+constexpr uint32_t kBc4WaveBlocks = 4096;
+
 hipError_t launch_bc4_blocks(const float *blocks, uint32_t n, void *dst, hipStream_t s)
 {
+    if (n < kBc4WaveBlocks) {
+        hipLaunchKernelGGL(bc4_blocks_wave_kernel, dim3(n), dim3(64), 0, s, blocks, n, (uint64_t *)dst);
+        return hipGetLastError();
+    }
     const uint32_t wg = 256, grid = (n + wg - 1) / wg;
     hipLaunchKernelGGL(bc4_blocks_kernel, dim3(grid), dim3(wg), 0, s, blocks, n, (uint64_t *)dst);
     return hipGetLastError();

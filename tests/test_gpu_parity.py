@@ -267,6 +267,31 @@ def test_bc23_images(gpu, fmt):
         assert np.array_equal(out, ref), _mismatch_report(out, ref)
 
 
+@pytest.mark.parametrize("n", [97, 4100])
+def test_bc4_block_batch_f32(gpu, n):
+    """Block-level BC4 (the batched Image_CompressAMDAlphaSingleModeBlock): below
+    4096 blocks one wave per block (bc4_blocks_wave_kernel, the grid and climb
+    spread over the lanes), from 4096 one lane per block; both bit-exact vs the
+    oracle on noise, 8-bit grid values, solid and two-value blocks and blocks at
+    the FIXED-mode extremes (0 / 1)."""
+    import torch
+    rng = np.random.default_rng(n)
+    v = rng.random((n, 16), dtype=np.float32)
+    v[::3] = np.round(v[::3] * 255) / np.float32(255.0)
+    v[1::7] = v[1::7, :1]                                            # solid
+    v[2::7] = np.where(rng.random((len(v[2::7]), 16)) < 0.5, v[2::7, :1], v[2::7, 1:2])   # two values
+    v[3::7, :5] = 0.0                                                # extremes: 6-value mode's fixed 0 / 255
+    v[3::7, 5:9] = 1.0
+    v[4::7] = v[4::7] * np.float32(0.15) + np.float32(0.4)          # narrow range: climb without the grid
+    t = torch.from_numpy(v).cuda()
+    dst = torch.zeros(n * 8, dtype=torch.uint8, device="cuda")
+    gic.encode_blocks_f32(gic.FMT_BC4, t, dst)
+    torch.cuda.synchronize()
+    got = dst.cpu().numpy().reshape(-1, 8)
+    for i in range(n):
+        assert got[i].tobytes() == oracle_lib.bc4_block(v[i]), i
+
+
 @pytest.mark.parametrize("fmt", [2, 3])
 def test_bc23_block_batch_f32(gpu, fmt):
     """Block-level BC2/BC3 on arbitrary float blocks (the batched form of the
