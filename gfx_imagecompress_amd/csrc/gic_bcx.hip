@@ -212,11 +212,33 @@ __device__ __forceinline__ float ramp_fit_error(const Col &u, const float r[3][4
     return err;
 }
 
+// ---- wave-cooperative searches (one 64-lane wave per block: small batches,
+// the block-level entry points).  Every lane holds the block; a search's
+// candidates are spread over the lanes and the sequential choice -- the first
+// strictly smaller error in loop order -- is recovered by an (error, order)
+// minimum over the wave.  Each candidate's error is the same function of the
+// same floats as in the lane-per-block loop, so the blocks are bit-identical.
+
+// (e, order) of the lane with the smallest e, ties to the smallest order; a lane
+// without a candidate brings e = +inf
+__device__ __forceinline__ void wave_argmin(float &e, int &o)
+{
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        const float e2 = __shfl_xor(e, m);
+        const int o2 = __shfl_xor(o, m);
+        if (e2 < e || (e2 == e && o2 < o)) {
+            e = e2;
+            o = o2;
+        }
+    }
+}
+
 // Refine, amd_bcx_body.cpp:582-806 (R, then G, then B 3x3 jitter of both
 // endpoints on the 565 grid; RefinementSteps = `steps`).  One pass per
 // channel, a template on the channel so every index is static (a runtime
 // channel loop does not unroll and turns each array access into selects).
-template <int N, int CH, class Col>
+template <int N, int CH, bool WAVE = false, class Col>
 __device__ __forceinline__ void refine_pass(float cur[3][2], const float base[3][2], const Col &u, int lo, int hi,
                                             float &best)
 {
@@ -246,6 +268,45 @@ __device__ __forceinline__ void refine_pass(float cur[3][2], const float base[3]
     const float grid = (float)(1 << (8 - chan_bits(CH)));
     const float wc = (CH == CH_R) ? wr : (CH == CH_G) ? wg : wb;
     float b0 = base[CH][0], b1 = base[CH][1];
+    if constexpr (WAVE) {
+        // candidate t = (a - lo) * span + (b - lo) on lane t % 64
+        const int span = hi - lo + 1, ln = (int)(threadIdx.x & 63u);
+        float be = __builtin_huge_valf();
+        int bo = 0x7fffffff;
+        for (int t = ln; t < span * span; t += 64) {
+            const int a = lo + t / span, b = lo + t % span;
+            cur[CH][0] = minr(maxr(base[CH][0] + (float)a * grid, 0.f), 255.f);
+            cur[CH][1] = minr(maxr(base[CH][1] + (float)b * grid, 0.f), 255.f);
+            const bool flat = expand_grid(wk, cur);
+            chan_ramp<N>(r[CH], wk[CH]);
+            float mse = 0.f;
+            const int nr = flat ? 1 : N;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                float m = 10000000.f;
+#pragma unroll
+                for (int k = 0; k < N; ++k) {
+                    float d = r[CH][k] - u.c(i, CH);
+                    float e = side[k][i] + d * d * wc;
+                    m = (k < nr) ? minr(m, e) : m;
+                }
+                mse += m * u.rpt(i);
+            }
+            if (mse < best && mse < be) {
+                be = mse;
+                bo = t;
+            }
+        }
+        wave_argmin(be, bo);
+        if (bo != 0x7fffffff) {
+            b0 = minr(maxr(base[CH][0] + (float)(lo + bo / span) * grid, 0.f), 255.f);
+            b1 = minr(maxr(base[CH][1] + (float)(lo + bo % span) * grid, 0.f), 255.f);
+            best = be;
+        }
+        cur[CH][0] = b0;
+        cur[CH][1] = b1;
+        return;
+    }
     for (int a = lo; a <= hi; ++a)
         for (int b = lo; b <= hi; ++b) {
             cur[CH][0] = minr(maxr(base[CH][0] + (float)a * grid, 0.f), 255.f);
@@ -354,7 +415,7 @@ __device__ __forceinline__ void refine_pass3(float cur[3][2], const float base[3
     cur[CH][1] = b1;
 }
 
-template <int N, class Col>
+template <int N, bool WAVE = false, class Col>
 __device__ __forceinline__ void refine_channels(float cur[3][2], const Col &u, int steps)
 {
     float base[3][2], wk[3][2], r[3][4];
@@ -377,9 +438,9 @@ __device__ __forceinline__ void refine_channels(float cur[3][2], const Col &u, i
         refine_pass3<N, CH_B>(cur, base, u, best);
     } else {
         const auto &ur = regs(u);
-        refine_pass<N, CH_R>(cur, base, ur, lo, hi, best);
-        refine_pass<N, CH_G>(cur, base, ur, lo, hi, best);
-        refine_pass<N, CH_B>(cur, base, ur, lo, hi, best);
+        refine_pass<N, CH_R, WAVE>(cur, base, ur, lo, hi, best);
+        refine_pass<N, CH_G, WAVE>(cur, base, ur, lo, hi, best);
+        refine_pass<N, CH_B, WAVE>(cur, base, ur, lo, hi, best);
     }
 }
 
@@ -601,9 +662,10 @@ __device__ __forceinline__ float last_colour(const Col &u, int j)
 }
 
 // CompressRGBBlockX, amd_bcx_body.cpp:937-1203
-template <int N, bool R3D, class Col>
+template <int N, bool R3D, bool WAVE = false, class Col>
 __device__ __forceinline__ void fit_endpoints(float result[3][2], const Col &u, int steps)
 {
+    static_assert(!(WAVE && R3D), "the wave searches cover Refine, not Refine3D");
     float rc[3][2];
     bool done = false;
     if (u.n <= 2) {
@@ -666,6 +728,26 @@ __device__ __forceinline__ void fit_endpoints(float result[3][2], const Col &u, 
             // 8x8 endpoint candidates, endpoints advanced by repeated adds
             // exactly as the reference loop does (:1095-1097)
             float err = 128000.f, pos0 = 0.f, pos1 = 0.f;
+            if constexpr (WAVE) {
+                // candidate (l, h) on lane 8 l + h
+                const int ln = (int)(threadIdx.x & 63u);
+                float lp = ls, hp = he;
+                for (int k = 0; k < (ln >> 3); ++k) lp += stp;
+                for (int k = 0; k < (ln & 7); ++k) hp -= stp;
+                const RampStep rs = ramp_step<N>(lp, hp);
+                float e = proj_ramp_error<8, 16>(proj_ramp_error<0, 8>(0.f, prj, perr, prem, rs), prj, perr, prem, rs);
+                int o = ln;
+                if (!(e < err)) {
+                    e = __builtin_huge_valf();
+                    o = 0x7fffffff;
+                }
+                wave_argmin(e, o);
+                if (o != 0x7fffffff) {
+                    err = e;
+                    pos0 = __shfl(lp, o);
+                    pos1 = __shfl(hp, o);
+                }
+            } else {
             float lp = ls;
             for (int l = 0; l < 8; ++l, lp += stp) {
                 float hp = he;
@@ -682,6 +764,7 @@ __device__ __forceinline__ void fit_endpoints(float result[3][2], const Col &u, 
                         pos1 = hp;
                     }
                 }
+            }
             }
             pos0 = pos0 * (scl1 - scl0) + scl0;
             pos1 = pos1 * (scl1 - scl0) + scl0;
@@ -740,7 +823,7 @@ __device__ __forceinline__ void fit_endpoints(float result[3][2], const Col &u, 
     if (R3D)
         refine_3d<N>(result, regs(u), steps);
     else
-        refine_channels<N>(result, u, steps);
+        refine_channels<N, WAVE>(result, u, steps);
 }
 
 // Leaders and ranks of the kept texels' colour keys: a kept texel leads its
@@ -986,7 +1069,7 @@ __device__ __forceinline__ uint32_t final_indices(const Tex &tex, const uint8_t 
 
 // CompRGBABlock, amd_bcx_body.cpp:1209-1297.  Returns the float error (FLT_MAX
 // for a 4-colour ramp over transparent texels).
-template <int N, bool R3D = false, class Col, class Tex>
+template <int N, bool R3D = false, bool WAVE = false, class Col, class Tex>
 __device__ __forceinline__ float comp_rgba(const Tex &t, int steps, bool use_alpha, uint8_t ep[3][2], uint32_t &ibits,
                                            const Col &u, int kept)
 {
@@ -1001,7 +1084,7 @@ __device__ __forceinline__ float comp_rgba(const Tex &t, int steps, bool use_alp
     }
     if (kept != 16 && use_alpha && !(N & 1)) return 3.402823466e+38f;
     float res[3][2];
-    fit_endpoints<N, R3D>(res, u, steps);
+    fit_endpoints<N, R3D, WAVE>(res, u, steps);
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
         ep[ch][0] = (uint8_t)res[ch][0];
@@ -1032,7 +1115,7 @@ __device__ __forceinline__ uint2 pack_bc1(const uint8_t ep[3][2], uint32_t ibits
 // Image_CompressAMDBC1Block, amd_bcx_helpers.cpp:51-105.  The 3-colour result is
 // packed into its block words before the 4-colour search runs, so only those two
 // words and its error stay live across it.
-template <bool R3D, class Col, class Tex>
+template <bool R3D, bool WAVE = false, class Col, class Tex>
 __device__ __forceinline__ uint2 encode_bc1(const Col &u, int kept, const Tex &t, int steps, bool use_alpha)
 {
     uint2 b3;
@@ -1040,14 +1123,14 @@ __device__ __forceinline__ uint2 encode_bc1(const Col &u, int kept, const Tex &t
     {
         uint8_t ep3[3][2];
         uint32_t i3 = 0;
-        e3f = comp_rgba<3, R3D>(t, steps, use_alpha, ep3, i3, u, kept);
+        e3f = comp_rgba<3, R3D, WAVE>(t, steps, use_alpha, ep3, i3, u, kept);
         b3 = pack_bc1(ep3, i3, false);
     }
     const double e3 = e3f;
     if (e3 == 0.0) return b3;
     uint8_t ep4[3][2];
     uint32_t i4 = 0;
-    const double e4 = comp_rgba<4, R3D>(t, steps, use_alpha, ep4, i4, u, kept);
+    const double e4 = comp_rgba<4, R3D, WAVE>(t, steps, use_alpha, ep4, i4, u, kept);
     const bool m4 = !(e3 <= e4);
     return m4 ? pack_bc1(ep4, i4, true) : b3;
 }
@@ -1110,7 +1193,7 @@ __device__ __forceinline__ uint2 encode_bc1_u8_lds(const uint32_t px[16], int st
     return encode_bc1<R3D>(ul, kept, t, steps, use_alpha);
 }
 
-template <bool R3D>
+template <bool R3D, bool WAVE = false>
 __device__ __forceinline__ uint2 encode_bc1_f32(const float in[64], int steps, float thr01)
 {
     const bool use_alpha = thr01 > 0.0f;
@@ -1118,7 +1201,7 @@ __device__ __forceinline__ uint2 encode_bc1_f32(const float in[64], int steps, f
     int kept;
     unique_colours(u, in, use_alpha, thr01, kept);
     const TexF t{in, thr01 * 255.f};
-    return encode_bc1<R3D>(u, kept, t, steps, use_alpha);
+    return encode_bc1<R3D, WAVE>(u, kept, t, steps, use_alpha);
 }
 
 // --------------------------------------------------------- BC2 / BC3 ---
@@ -1132,12 +1215,12 @@ __device__ __forceinline__ uint2 encode_bc1_f32(const float in[64], int steps, f
 // reference's own 4-colour CompRGBABlock fit with alpha ignored (the BC1 path's
 // second candidate, amd_bcx_helpers.cpp:77-88), packed with c0 > c1 as
 // :164-171 (BC2/BC3 colour blocks are always 4-colour).
-template <bool R3D, class Col, class Tex>
+template <bool R3D, bool WAVE = false, class Col, class Tex>
 __device__ __forceinline__ uint2 encode_rgb4(const Col &u, int kept, const Tex &t, int steps)
 {
     uint8_t ep[3][2];
     uint32_t ib = 0;
-    comp_rgba<4, R3D>(t, steps, false, ep, ib, u, kept);
+    comp_rgba<4, R3D, WAVE>(t, steps, false, ep, ib, u, kept);
     const unsigned c0 = ((unsigned)(ep[CH_R][0] >> 3) << 11) | ((unsigned)(ep[CH_G][0] >> 2) << 5) |
                         (unsigned)(ep[CH_B][0] >> 3);
     const unsigned c1 = ((unsigned)(ep[CH_R][1] >> 3) << 11) | ((unsigned)(ep[CH_G][1] >> 2) << 5) |
@@ -1416,7 +1499,8 @@ __device__ float scalar_block(const float v[16], const float sorted[16], uint8_t
 
 // Image_CompressAMDAlphaSingleModeBlock + EncodeAlphaBlock,
 // amd_bcx_helpers.cpp:32-46, :125-140
-// ascending sort by rank (equal values are interchangeable)
+// ascending sort by rank, as encode_bc4 (the lane version keeps its own copy inline:
+// through a helper the image kernel's sort went to scratch)
 __device__ __forceinline__ void bc4_sort(const float v[16], float s[16])
 {
     bool nan = false;
@@ -1460,8 +1544,44 @@ __device__ __forceinline__ void bc4_sort(const float v[16], float s[16])
 template <class W = Bc4Scratch>
 __device__ uint64_t encode_bc4(const float v[16], W wk = W())
 {
+    // ascending sort by rank (equal values are interchangeable)
     float s[16];
-    bc4_sort(v, s);
+    bool nan = false;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) nan = nan || v[i] != v[i];
+    if (!nan) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            int r = 0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) r += (v[j] < v[i] || (v[j] == v[i] && j < i)) ? 1 : 0;
+            // scatter through a select chain keeps s[] in registers
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (r == k) s[k] = v[i];
+        }
+    } else {
+        // A NaN texel (float sources only): QSortFCmp (:1609-1618) calls a NaN
+        // equal to everything, which is no total order, so the reference's
+        // qsort result is undefined (C11 7.22.5p4) and ranks would leave holes.
+        // The order is the oracle's insertion sort's (orc_bcx.c
+        // scalar_endpoints): each value moves left past larger ones only, as
+        // a static chain of selects.
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[i] = v[i];
+#pragma unroll
+        for (int i = 1; i < 16; ++i) {
+            const float t = s[i];
+            bool go = true;
+#pragma unroll
+            for (int j = i - 1; j >= 0; --j) {
+                const bool mv = go && (s[j] - t) > 0.0f;
+                s[j + 1] = mv ? s[j] : (go ? t : s[j + 1]);
+                go = mv;
+            }
+            s[0] = go ? t : s[0];
+        }
+    }
     uint8_t ep8[2], ep6[2];
     uint64_t i8, i6 = 0;
     const float e8 = scalar_block<8, false>(v, s, ep8, i8, wk);
@@ -1481,21 +1601,6 @@ __device__ uint64_t encode_bc4(const float v[16], W wk = W())
 // the sequential choice -- the first strictly smaller error in loop order -- is
 // recovered by a (error, order) minimum.  Every ramp error is the same function
 // of the same floats as in scalar_endpoints, so the blocks are bit-identical.
-
-// (e, order) of the lane with the smallest e, ties to the smallest order; a lane
-// without a candidate brings e = +inf
-__device__ __forceinline__ void wave_argmin(float &e, int &o)
-{
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1) {
-        const float e2 = __shfl_xor(e, m);
-        const int o2 = __shfl_xor(o, m);
-        if (e2 < e || (e2 == e && o2 < o)) {
-            e = e2;
-            o = o2;
-        }
-    }
-}
 
 template <int N, bool FIXED>
 __device__ void scalar_endpoints_wave(float ramp[2], const float vals_sorted[16], float *uv, float *ur)
@@ -1783,7 +1888,45 @@ __global__ void __launch_bounds__(256) bc4_blocks_kernel(const float *__restrict
     dst[id] = bcx::encode_bc4(v);
 }
 
-// one 64-lane workgroup (one wave) per block: small batches
+// one 64-lane workgroup (one wave) per block: small batches (Refine only)
+__global__ void __launch_bounds__(64) bc1_blocks_wave_kernel(const float *__restrict__ blocks, uint32_t n, Bc1Params p,
+                                                             uint2 *__restrict__ dst)
+{
+    const uint32_t id = blockIdx.x;
+    if (id >= n) return;
+    float blk[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) blk[i] = blocks[(size_t)id * 64 + i];
+    const uint2 b = bcx::encode_bc1_f32<false, true>(blk, p.steps, p.alpha_threshold);
+    if (threadIdx.x == 0) dst[id] = b;
+}
+
+__global__ void __launch_bounds__(64) bc23_blocks_wave_kernel(const float *__restrict__ blocks, uint32_t n, int fmt,
+                                                              Bc1Params p, uint4 *__restrict__ dst)
+{
+    __shared__ float uv[16], ur[16];
+    const uint32_t id = blockIdx.x;
+    if (id >= n) return;
+    float blk[64], v[16];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) blk[i] = blocks[(size_t)id * 64 + i];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = blk[i * 4 + 3];
+    uint2 a;
+    if (fmt == 3) {
+        const uint64_t r = bcx::encode_bc4_wave(v, uv, ur);
+        a = make_uint2((uint32_t)r, (uint32_t)(r >> 32));
+    } else {
+        a = bcx::encode_explicit_alpha_f32(v);
+    }
+    bcx::ColF u;
+    int kept;
+    bcx::unique_colours(u, blk, false, 0.f, kept);
+    const bcx::TexF t{blk, 0.f};
+    const uint2 c = bcx::encode_rgb4<false, true>(u, kept, t, p.steps);
+    if (threadIdx.x == 0) dst[id] = make_uint4(a.x, a.y, c.x, c.y);
+}
+
 __global__ void __launch_bounds__(64) bc4_blocks_wave_kernel(const float *__restrict__ blocks, uint32_t n,
                                                              uint64_t *__restrict__ dst)
 {
@@ -2083,9 +2226,18 @@ hipError_t launch_bc23_image(const Geometry &g, int fmt, int steps, int force_al
     return hipGetLastError();
 }
 
+// Below this many blocks a wave per block (the *_wave_kernel launches) finishes
+// sooner than a lane per block: the batch cannot fill the chip lane-wise, and a
+// block's serial search is the call's latency.
+constexpr uint32_t kWaveBlocks = 4096;
+
 hipError_t launch_bc23_blocks(const float *blocks, uint32_t n, int fmt, int steps, int r3d, void *dst, hipStream_t s)
 {
     const Bc1Params p{0.f, steps, 0, 0u, 0u};
+    if (n < kWaveBlocks && !r3d) {
+        hipLaunchKernelGGL(bc23_blocks_wave_kernel, dim3(n), dim3(64), 0, s, blocks, n, fmt, p, (uint4 *)dst);
+        return hipGetLastError();
+    }
     const uint32_t wg = 256, grid = (n + wg - 1) / wg;
     if (r3d)
         hipLaunchKernelGGL(bc23_blocks_kernel<true>, dim3(grid), dim3(wg), 0, s, blocks, n, fmt, p, (uint4 *)dst);
@@ -2107,6 +2259,10 @@ hipError_t launch_bc45_image(const Geometry &g, int fmt, int channel, void *dst,
 hipError_t launch_bc1_blocks(const float *blocks, uint32_t n, float thr, int steps, int r3d, void *dst, hipStream_t s)
 {
     const Bc1Params p{thr, steps, 0, 0u, 0u};
+    if (n < kWaveBlocks && !r3d) {
+        hipLaunchKernelGGL(bc1_blocks_wave_kernel, dim3(n), dim3(64), 0, s, blocks, n, p, (uint2 *)dst);
+        return hipGetLastError();
+    }
     const uint32_t wg = 256, grid = (n + wg - 1) / wg;
     if (r3d)
         hipLaunchKernelGGL(bc1_blocks_kernel<true>, dim3(grid), dim3(wg), 0, s, blocks, n, p, (uint2 *)dst);
@@ -2115,14 +2271,9 @@ hipError_t launch_bc1_blocks(const float *blocks, uint32_t n, float thr, int ste
     return hipGetLastError();
 }
 
-// Below this many blocks a wave per block (bc4_blocks_wave_kernel) finishes
-// sooner than a lane per block: the batch cannot fill the chip lane-wise, and a
-// block's serial search is the call's latency.
-constexpr uint32_t kBc4WaveBlocks = 4096;
-
 hipError_t launch_bc4_blocks(const float *blocks, uint32_t n, void *dst, hipStream_t s)
 {
-    if (n < kBc4WaveBlocks) {
+    if (n < kWaveBlocks) {
         hipLaunchKernelGGL(bc4_blocks_wave_kernel, dim3(n), dim3(64), 0, s, blocks, n, (uint64_t *)dst);
         return hipGetLastError();
     }

@@ -292,17 +292,42 @@ def test_bc4_block_batch_f32(gpu, n):
         assert got[i].tobytes() == oracle_lib.bc4_block(v[i]), i
 
 
-@pytest.mark.parametrize("fmt", [2, 3])
-def test_bc23_block_batch_f32(gpu, fmt):
-    """Block-level BC2/BC3 on arbitrary float blocks (the batched form of the
-    component-block API, Image_CompressAMDRGBSingleModeBlock / ...AlphaSingleModeBlock)."""
+@pytest.mark.parametrize("n", [97, 4100])
+@pytest.mark.parametrize("steps,thr", [(1, 0.0), (1, 128 / 255.0), (2, 0.5)])
+def test_bc1_block_batch_f32(gpu, n, steps, thr):
+    """Block-level BC1 (the batched Image_CompressAMDBC1Block): below 4096 blocks
+    one wave per block (bc1_blocks_wave_kernel: the 8x8 endpoint candidates on
+    the wave's lanes, each Refine channel pass's (2 steps + 1)^2 jitters spread
+    over them), from 4096 one lane per block; bit-exact vs the oracle on noise,
+    8-bit grid values, solid blocks, alpha below / above the threshold."""
     import torch
-    rng = np.random.default_rng(fmt)
-    blocks = rng.random((96, 16, 4), dtype=np.float32)
+    rng = np.random.default_rng(1000 * steps + n)
+    blocks = rng.random((n, 16, 4), dtype=np.float32)
+    blocks[::3] = np.round(blocks[::3] * 255) / np.float32(255.0)
+    blocks[1::5] = blocks[1::5, :1]                      # solid blocks
+    blocks[2::5, :, 3] = 1.0                             # opaque
+    t = torch.from_numpy(blocks.reshape(-1, 64)).cuda()
+    dst = torch.zeros(n * 8, dtype=torch.uint8, device="cuda")
+    gic.encode_blocks_f32(gic.FMT_BC1, t, dst, gic.Options(refinement_steps=steps, bc1_alpha_threshold=thr))
+    torch.cuda.synchronize()
+    got = dst.cpu().numpy().reshape(-1, 8)
+    for i in range(n):
+        assert got[i].tobytes() == oracle_lib.bc1_block(blocks[i], steps=steps, threshold=thr), i
+
+
+@pytest.mark.parametrize("n", [96, 4100])
+@pytest.mark.parametrize("fmt", [2, 3])
+def test_bc23_block_batch_f32(gpu, fmt, n):
+    """Block-level BC2/BC3 on arbitrary float blocks (the batched form of the
+    component-block API, Image_CompressAMDRGBSingleModeBlock / ...AlphaSingleModeBlock):
+    a wave per block below 4096 blocks, a lane per block from 4096."""
+    import torch
+    rng = np.random.default_rng(fmt + n)
+    blocks = rng.random((n, 16, 4), dtype=np.float32)
     blocks[::3] = np.round(blocks[::3] * 255) / np.float32(255.0)
     blocks[1::5] = blocks[1::5, :1]                      # solid blocks
     t = torch.from_numpy(blocks.reshape(-1, 64)).cuda()
-    dst = torch.zeros(96 * 16, dtype=torch.uint8, device="cuda")
+    dst = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
     gic.encode_blocks_f32(fmt, t, dst)
     torch.cuda.synchronize()
     got = dst.cpu().numpy().reshape(-1, 16)

@@ -1,0 +1,11 @@
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r04x; mkdir -p $O
+cd $R
+export LD_LIBRARY_PATH=$R/gfx_imagecompress_amd/lib
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_capi.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -4 $O/tests.log
+timeout -k 10 120 ./gpurun_dbg/block_latency 2000 > $O/lat.txt 2>&1 || exit 1
+cat $O/lat.txt
+timeout -k 10 120 python3 tools/time_bc45.py > $O/bc45.txt 2>&1 || exit 1
+grep -v amdgpu.ids $O/bc45.txt
