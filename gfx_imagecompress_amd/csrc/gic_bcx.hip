@@ -1888,43 +1888,82 @@ __global__ void __launch_bounds__(256) bc4_blocks_kernel(const float *__restrict
     dst[id] = bcx::encode_bc4(v);
 }
 
-// one 64-lane workgroup (one wave) per block: small batches (Refine only)
-__global__ void __launch_bounds__(64) bc1_blocks_wave_kernel(const float *__restrict__ blocks, uint32_t n, Bc1Params p,
-                                                             uint2 *__restrict__ dst)
+// Small batches (Refine only): one block per 128-thread workgroup, two waves --
+// wave 0 runs the 3-colour search, wave 1 the 4-colour one (independent until
+// encode_bc1's comparison, amd_bcx_helpers.cpp:51-105), each search spread over
+// its wave's lanes.
+__global__ void __launch_bounds__(128) bc1_blocks_wave_kernel(const float *__restrict__ blocks, uint32_t n, Bc1Params p,
+                                                              uint2 *__restrict__ dst)
 {
+    __shared__ uint2 res[2];
+    __shared__ float err[2];
     const uint32_t id = blockIdx.x;
     if (id >= n) return;
     float blk[64];
 #pragma unroll
     for (int i = 0; i < 64; ++i) blk[i] = blocks[(size_t)id * 64 + i];
-    const uint2 b = bcx::encode_bc1_f32<false, true>(blk, p.steps, p.alpha_threshold);
-    if (threadIdx.x == 0) dst[id] = b;
-}
-
-__global__ void __launch_bounds__(64) bc23_blocks_wave_kernel(const float *__restrict__ blocks, uint32_t n, int fmt,
-                                                              Bc1Params p, uint4 *__restrict__ dst)
-{
-    __shared__ float uv[16], ur[16];
-    const uint32_t id = blockIdx.x;
-    if (id >= n) return;
-    float blk[64], v[16];
-#pragma unroll
-    for (int i = 0; i < 64; ++i) blk[i] = blocks[(size_t)id * 64 + i];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = blk[i * 4 + 3];
-    uint2 a;
-    if (fmt == 3) {
-        const uint64_t r = bcx::encode_bc4_wave(v, uv, ur);
-        a = make_uint2((uint32_t)r, (uint32_t)(r >> 32));
-    } else {
-        a = bcx::encode_explicit_alpha_f32(v);
-    }
+    const float thr01 = p.alpha_threshold;
+    const bool use_alpha = thr01 > 0.0f;
     bcx::ColF u;
     int kept;
-    bcx::unique_colours(u, blk, false, 0.f, kept);
-    const bcx::TexF t{blk, 0.f};
-    const uint2 c = bcx::encode_rgb4<false, true>(u, kept, t, p.steps);
-    if (threadIdx.x == 0) dst[id] = make_uint4(a.x, a.y, c.x, c.y);
+    bcx::unique_colours(u, blk, use_alpha, thr01, kept);
+    const bcx::TexF t{blk, thr01 * 255.f};
+    const int w = (int)(threadIdx.x >> 6);
+    uint8_t ep[3][2];
+    uint32_t ib = 0;
+    float e;
+    uint2 b;
+    if (w == 0) {
+        e = bcx::comp_rgba<3, false, true>(t, p.steps, use_alpha, ep, ib, u, kept);
+        b = bcx::pack_bc1(ep, ib, false);
+    } else {
+        e = bcx::comp_rgba<4, false, true>(t, p.steps, use_alpha, ep, ib, u, kept);
+        b = bcx::pack_bc1(ep, ib, true);
+    }
+    if ((threadIdx.x & 63u) == 0) {
+        res[w] = b;
+        err[w] = e;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double e3 = err[0], e4 = err[1];
+        dst[id] = (e3 == 0.0 || e3 <= e4) ? res[0] : res[1];
+    }
+}
+
+// the same for BC2 / BC3: wave 0 the colour half, wave 1 the alpha half
+__global__ void __launch_bounds__(128) bc23_blocks_wave_kernel(const float *__restrict__ blocks, uint32_t n, int fmt,
+                                                               Bc1Params p, uint4 *__restrict__ dst)
+{
+    __shared__ float uv[16], ur[16];
+    __shared__ uint2 res[2];
+    const uint32_t id = blockIdx.x;
+    if (id >= n) return;
+    float blk[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) blk[i] = blocks[(size_t)id * 64 + i];
+    const int w = (int)(threadIdx.x >> 6);
+    uint2 r2;
+    if (w == 1) {
+        float v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = blk[i * 4 + 3];
+        if (fmt == 3) {
+            const uint64_t r = bcx::encode_bc4_wave(v, uv, ur);
+            r2 = make_uint2((uint32_t)r, (uint32_t)(r >> 32));
+        } else {
+            r2 = bcx::encode_explicit_alpha_f32(v);
+        }
+    } else {
+        bcx::ColF u;
+        int kept;
+        bcx::unique_colours(u, blk, false, 0.f, kept);
+        const bcx::TexF t{blk, 0.f};
+        r2 = bcx::encode_rgb4<false, true>(u, kept, t, p.steps);
+    }
+    if ((threadIdx.x & 63u) == 0) res[w] = r2;
+    __syncthreads();
+    if (threadIdx.x == 0) dst[id] = make_uint4(res[1].x, res[1].y, res[0].x, res[0].y);
 }
 
 __global__ void __launch_bounds__(64) bc4_blocks_wave_kernel(const float *__restrict__ blocks, uint32_t n,
@@ -2235,7 +2274,7 @@ hipError_t launch_bc23_blocks(const float *blocks, uint32_t n, int fmt, int step
 {
     const Bc1Params p{0.f, steps, 0, 0u, 0u};
     if (n < kWaveBlocks && !r3d) {
-        hipLaunchKernelGGL(bc23_blocks_wave_kernel, dim3(n), dim3(64), 0, s, blocks, n, fmt, p, (uint4 *)dst);
+        hipLaunchKernelGGL(bc23_blocks_wave_kernel, dim3(n), dim3(128), 0, s, blocks, n, fmt, p, (uint4 *)dst);
         return hipGetLastError();
     }
     const uint32_t wg = 256, grid = (n + wg - 1) / wg;
@@ -2260,7 +2299,7 @@ hipError_t launch_bc1_blocks(const float *blocks, uint32_t n, float thr, int ste
 {
     const Bc1Params p{thr, steps, 0, 0u, 0u};
     if (n < kWaveBlocks && !r3d) {
-        hipLaunchKernelGGL(bc1_blocks_wave_kernel, dim3(n), dim3(64), 0, s, blocks, n, p, (uint2 *)dst);
+        hipLaunchKernelGGL(bc1_blocks_wave_kernel, dim3(n), dim3(128), 0, s, blocks, n, p, (uint2 *)dst);
         return hipGetLastError();
     }
     const uint32_t wg = 256, grid = (n + wg - 1) / wg;
