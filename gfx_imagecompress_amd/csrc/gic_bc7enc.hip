@@ -854,6 +854,35 @@ __device__ __forceinline__ uint32_t pick_partition(const uint32_t px[16], const 
     return best_part;
 }
 
+// pick_partition with the shapes' estimates on the lanes of a wave (one block per
+// wave, every lane holding it): lane it sums shape kEncPartOrder[it] in full, then
+// the reference's sequential choice (filter bank, stop rules, '<' keeps the
+// first) runs over those totals -- full sums are equivalent (see estimate2).
+template <bool P>
+__device__ __forceinline__ uint32_t pick_partition_wave(const uint32_t px[16], const Ycc &tx, const EncCfg &cf)
+{
+    const uint32_t total = cf.max_parts < 64 ? cf.max_parts : 64;
+    if (total <= 1) return 0;
+    const uint32_t ln = threadIdx.x & 63u;
+    uint32_t el = kNone;
+    if (ln < total) el = estimate2<P>(shape_mask(kBc7Shape2[kEncPartOrder[ln]], 0), px, tx, cf, kNone);
+    uint32_t best = kNone, best_part = 0, key = 0;
+    bool stop = false;
+    for (uint32_t it = 0; it < total; ++it) {
+        if (stop || best == 0) break;
+        const uint32_t part = kEncPartOrder[it];
+        if (cf.filterbank && it >= 14 && it <= 34 && !(kEncPredictors[part] & (1u << (key + 1)))) {
+            if (it == 34) stop = true;
+            continue;
+        }
+        const uint32_t e = (uint32_t)__shfl((int)el, (int)it);
+        if (e < best) best = e, best_part = part;
+        if (part == 34 && best_part != 34) stop = true;
+        if (it == 13) key = best_part;
+    }
+    return best_part;
+}
+
 // 128-bit little-endian bit writer (set_block_bits :1283-1295)
 struct Bits {
     uint64_t w0 = 0, w1 = 0;
@@ -923,7 +952,7 @@ __device__ __forceinline__ uint4 pack_block(bool mode1, uint32_t part, uint64_t 
 // bc7enc16_compress_block :1517-1547 with handle_alpha_block / handle_opaque_block
 // :1390-1515 (m_endpoints_share_pbit, uninitialised for alpha blocks in the
 // reference, is false: mode 6 has a p-bit per endpoint)
-template <bool P>
+template <bool P, bool WAVE = false>
 __device__ __forceinline__ uint4 encode_block(const uint32_t px[16], const EncCfg &cf, const EncLds &L, Ycc tx)
 {
     if (P) {
@@ -948,7 +977,7 @@ __device__ __forceinline__ uint4 encode_block(const uint32_t px[16], const EncCf
     if (!alpha && r6[0].err > 0 && cf.max_parts > 0) {
         // mode 1 on the partition the estimator picks, both subsets at once (the
         // reference stops after the first subset if it alone loses: equivalent)
-        part = pick_partition<P>(px, tx, cf);
+        part = WAVE ? pick_partition_wave<P>(px, tx, cf) : pick_partition<P>(px, tx, cf);
         const uint32_t m0 = shape_mask(kBc7Shape2[part], 0);
         Prob p1[2];
 #pragma unroll
@@ -1034,6 +1063,28 @@ __global__ void __launch_bounds__(256, GIC_ENC_WAVES) bc7enc_blocks_kernel(const
     dst[id] = encode_block<P>(px, cf, L, tx);
 }
 
+// small batches (the block-level entry point): one block per 64-lane wave, the
+// mode-1 partition estimates on the lanes (pick_partition_wave)
+template <bool P>
+__global__ void __launch_bounds__(64) bc7enc_blocks_wave_kernel(const uint4 *__restrict__ blocks, uint32_t n, EncCfg cf,
+                                                                uint4 *__restrict__ dst)
+{
+    __shared__ EncLds L;
+    __shared__ int ytab[P ? 48 * kYccStride : 1];
+    load_tables(L);
+    const Ycc tx{(uint32_t)(uintptr_t)(const __attribute__((address_space(3))) int *)(ytab + (P ? threadIdx.x : 0))};
+    const uint32_t id = blockIdx.x;
+    if (id >= n) return;
+    uint32_t px[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint4 v = blocks[(size_t)id * 4 + q];
+        px[q * 4 + 0] = v.x, px[q * 4 + 1] = v.y, px[q * 4 + 2] = v.z, px[q * 4 + 3] = v.w;
+    }
+    const uint4 b = encode_block<P, true>(px, cf, L, tx);
+    if (threadIdx.x == 0) dst[id] = b;
+}
+
 // float RGBA blocks (the gic_hip_encode_rows_src / block-ABI path): each texel
 // to RGBA8 as saturate(v) * 255 + 0.5 truncated (TinyImageFormat's UNORM8 encode
 // is un-vendored; this rounding is unpinned and is the identity on v / 255.0f)
@@ -1098,6 +1149,15 @@ hipError_t launch_bc7enc_image(const Geometry &g, const gic_options &o, void *ds
 hipError_t launch_bc7enc_blocks_u8(const uint32_t *blocks, uint32_t n, const gic_options &o, void *dst, hipStream_t s)
 {
     const EncCfg cf = make_cfg(o);
+    if (n < 4096) {   // a wave per block below 4096 blocks, as the BC1-BC4 block launches
+        if (o.bc7enc_perceptual)
+            hipLaunchKernelGGL(bc7enc_blocks_wave_kernel<true>, dim3(n), dim3(64), 0, s, (const uint4 *)blocks, n, cf,
+                               (uint4 *)dst);
+        else
+            hipLaunchKernelGGL(bc7enc_blocks_wave_kernel<false>, dim3(n), dim3(64), 0, s, (const uint4 *)blocks, n, cf,
+                               (uint4 *)dst);
+        return hipGetLastError();
+    }
     const uint32_t wg = 256, grid = (n + wg - 1) / wg;
     if (o.bc7enc_perceptual)
         hipLaunchKernelGGL(bc7enc_blocks_kernel<true>, dim3(grid), dim3(wg), 0, s, (const uint4 *)blocks, n, cf,

@@ -63,13 +63,16 @@ def test_bc7enc_image_matches_oracle(gpu, kind, fast, perceptual):
     assert np.array_equal(got, ref), _mismatch_report(got, ref)
 
 
+@pytest.mark.parametrize("n", [2048, 4200])
 @pytest.mark.parametrize("fast,perceptual", SETTINGS)
 @pytest.mark.parametrize("alpha", [False, True])
-def test_bc7enc_block_batch_matches_oracle(gpu, alpha, fast, perceptual):
-    """The block ABI (Image_CompressRichGel999BC7enc16) on 2048 seeded blocks:
-    random, low-contrast and two-colour blocks, opaque or with alpha."""
+def test_bc7enc_block_batch_matches_oracle(gpu, alpha, fast, perceptual, n):
+    """The block ABI (Image_CompressRichGel999BC7enc16) on seeded blocks: random,
+    low-contrast and two-colour blocks, opaque or with alpha.  Below 4096 blocks
+    a wave per block (the mode-1 partition estimates on its lanes), from 4096 a
+    lane per block."""
     import torch
-    blocks = _random_blocks(2048, 7 + alpha, alpha)
+    blocks = _random_blocks(n, 7 + alpha, alpha)
     src = torch.from_numpy(blocks.reshape(-1, 64)).cuda()
     dst = torch.zeros(blocks.shape[0] * 16, dtype=torch.uint8, device="cuda")
     gic.encode_blocks_u8(src, dst, gic.Options.bc7enc16(fast, perceptual))
