@@ -22,7 +22,8 @@ from dataclasses import dataclass, replace
 __all__ = [
     "GicError", "Options", "FMT_BC1", "FMT_BC2", "FMT_BC3", "FMT_BC4", "FMT_BC5", "FMT_BC6H", "FMT_BC6H_SF",
     "FMT_BC7", "FMT_BC7ENC16", "compress_bc6h",
-    "library", "encode_blocks_u8", "compress_bc7_fast",
+    "library", "encode_blocks_u8", "compress_bc7_fast", "iter_cap_hits", "set_iter_cap", "nonterminating_loops",
+    "last_h4_report",
     "block_bytes", "blocks_shape", "encode_device", "encode_device_src", "encode_blocks_f32", "decode_device", "compress_bc1", "compress_bc2",
     "compress_bc3", "compress_bc4", "compress_bc5", "compress_bc7", "LIB_PATH",
 ]
@@ -170,6 +171,10 @@ def library() -> ctypes.CDLL:
     lib.gic_iter_cap_hits.restype = ctypes.c_int
     lib.gic_set_iter_cap.argtypes = [ctypes.c_int]
     lib.gic_set_iter_cap.restype = ctypes.c_int
+    lib.gic_nonterminating_loops.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    lib.gic_nonterminating_loops.restype = ctypes.c_int
+    lib.gic_last_h4_report.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+    lib.gic_last_h4_report.restype = ctypes.c_int
     _lib = lib
     return lib
 
@@ -183,9 +188,10 @@ def _check(rc: int) -> None:
 
 
 def iter_cap_hits(reset: bool = False) -> int:
-    """Quantiser loops the GPU stopped at the iteration cap on the current
-    device (gic_iter_cap_hits): blocks where the reference would
-    not have returned."""
+    """Quantiser loops stopped at the iteration cap on the current device
+    (gic_iter_cap_hits).  BC7: each stop marks its block, which
+    the same call encodes again through the uncapped general path (see
+    :func:`last_h4_report`); BC6H: the loop's per-loop cap."""
     n = ctypes.c_ulonglong(0)
     _check(library().gic_iter_cap_hits(ctypes.byref(n), 1 if reset else 0))
     return int(n.value)
@@ -195,6 +201,22 @@ def set_iter_cap(cap: int) -> None:
     """The iteration cap (rounds past the never-reset counter's exhaustion;
     < 0 restores the default 4096).  A test hook."""
     _check(library().gic_set_iter_cap(int(cap)))
+
+
+def nonterminating_loops(reset: bool = False) -> int:
+    """Quantiser loops proven cyclic (the reference would never return on
+    their blocks) on the current device (gic_nonterminating_loops)."""
+    n = ctypes.c_ulonglong(0)
+    _check(library().gic_nonterminating_loops(ctypes.byref(n), 1 if reset else 0))
+    return int(n.value)
+
+
+def last_h4_report() -> tuple[int, int]:
+    """(blocks re-run after a cap stop, loops proven cyclic) of this thread's
+    last BC7 call (gic_last_h4_report)."""
+    a, b = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    _check(library().gic_last_h4_report(ctypes.byref(a), ctypes.byref(b)))
+    return int(a.value), int(b.value)
 
 
 def block_bytes(fmt: int) -> int:

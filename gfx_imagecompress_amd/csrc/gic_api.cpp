@@ -52,6 +52,9 @@ hipError_t launch_bc6h_image(const Geometry &g, int is_signed, int force_alpha_o
                              hipStream_t s);
 hipError_t bc7_iter_cap(int cap, unsigned long long *hits, int reset);
 hipError_t bc6h_iter_cap(int cap, unsigned long long *hits, int reset);
+hipError_t bc7_nonterm(unsigned long long *n, int reset);
+hipError_t bc6h_nonterm(unsigned long long *n, int reset);
+void bc7_last_h4(uint32_t *rerun, uint32_t *nonterm);
 }  // namespace gic
 
 static bool is_bc6h(gic_format f) { return f == GIC_FMT_BC6H || f == GIC_FMT_BC6H_SF; }
@@ -88,6 +91,24 @@ extern "C" int gic_set_iter_cap(int cap)
     if (e == hipSuccess) e = gic::bc7_iter_cap(cap, nullptr, 0);
     if (e == hipSuccess) e = gic::bc6h_iter_cap(cap, nullptr, 0);
     return e == hipSuccess ? GIC_OK : hip_fail(e);
+}
+
+extern "C" int gic_nonterminating_loops(unsigned long long *loops, int reset)
+{
+    if (!loops) return GIC_EINVAL;
+    unsigned long long a = 0, b = 0;
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = gic::bc7_nonterm(&a, reset);
+    if (e == hipSuccess) e = gic::bc6h_nonterm(&b, reset);
+    if (e != hipSuccess) return hip_fail(e);
+    *loops = a + b;
+    return GIC_OK;
+}
+
+extern "C" int gic_last_h4_report(uint32_t *rerun_blocks, uint32_t *nonterminating_loops)
+{
+    gic::bc7_last_h4(rerun_blocks, nonterminating_loops);
+    return GIC_OK;
 }
 
 extern "C" const char *gic_version(void) { return "gfx_imagecompress_amd 0.1 (gfx950)"; }

@@ -256,12 +256,19 @@ __device__ __forceinline__ uint64_t pack_idx(const int idx[16], uint32_t mask)
     return v;
 }
 
-// Iteration cap, as gic_bc7.hip: optQuantAnD_f's requantisation
-// loop never resets try_two (amd_hdr_encode.cpp:1427-1601), so past its
-// exhaustion the reference loops until the state is stable; the GPU stops
-// g_iter_cap rounds later and counts the hit (gic_iter_cap_hits).
+// Iteration cap: optQuantAnD_f's requantisation loop never
+// resets try_two (amd_hdr_encode.cpp:1427-1601), so past its exhaustion the
+// reference loops until the state is stable -- forever on a cycling state.
+// The loop's state is the index vector alone, so once try_two < 0 a Brent
+// cycle check (the same in oracle/orc_bc6h.c) stops the loop exactly where a
+// revisited state proves the reference never returns (g_nonterm), and a loop
+// still running g_iter_cap rounds past the exhaustion within one loop stops
+// there (g_iter_hits; the oracle applies the same per-loop cap).  Both stops
+// depend only on the loop's starting state, which keeps the 4000-round
+// fast-forward below exact.
 __device__ int g_iter_cap = 4096;
 __device__ unsigned long long g_iter_hits = 0;
+__device__ unsigned long long g_nonterm = 0;
 
 // optQuantAnD_f (amd_hdr_encode.cpp:1427-1601), dimension 3, quality 1.0, over
 // the members of `mask` (data = din, texel-indexed).  Returns the error; idx
@@ -339,6 +346,8 @@ __device__ __forceinline__ float opt_quant_f(const float din[16][3], uint32_t ma
         }
         if (it) {
             bool done;
+            uint64_t cyc_saved = 0;
+            int cyc_have = 0, cyc_pow = 1, cyc_lam = 0, cyc_rounds = 0;
             do {
                 float q = 0, s = 0, t = 0;
 #pragma unroll
@@ -378,9 +387,22 @@ __device__ __forceinline__ float opt_quant_f(const float din[16][3], uint32_t ma
                         done = done && cnt == idx[k];
                         idx[k] = cnt;
                     }
-                if (try_two < -g_iter_cap) {   // H4: the reference loops until done once try_two < 0
-                    atomicAdd(&g_iter_hits, 1ull);
-                    break;
+                if (!done && try_two < 0) {   // H4: the reference loops until done once try_two < 0
+                    const uint64_t st = pack_idx(idx, mask);
+                    if (cyc_have && st == cyc_saved) {
+                        atomicAdd(&g_nonterm, 1ull);
+                        break;
+                    }
+                    if (++cyc_rounds > g_iter_cap) {
+                        atomicAdd(&g_iter_hits, 1ull);
+                        break;
+                    }
+                    if (!cyc_have || ++cyc_lam == cyc_pow) {
+                        cyc_saved = st;
+                        cyc_have = 1;
+                        cyc_pow <<= 1;
+                        cyc_lam = 0;
+                    }
                 }
             } while (!done && try_two--);
             if (it == 1) {
@@ -1559,6 +1581,16 @@ static hipError_t bc6h_run(const float *blocks, const Geometry *g, uint32_t n, i
     }
     const hipError_t ef = hipFreeAsync(mem, s);
     return e != hipSuccess ? e : ef;
+}
+
+hipError_t bc6h_nonterm(unsigned long long *n, int reset)
+{
+    hipError_t e = hipMemcpyFromSymbol(n, HIP_SYMBOL(bc6h::g_nonterm), sizeof(*n));
+    if (e == hipSuccess && reset) {
+        const unsigned long long z = 0;
+        e = hipMemcpyToSymbol(HIP_SYMBOL(bc6h::g_nonterm), &z, sizeof(z));
+    }
+    return e;
 }
 
 hipError_t bc6h_iter_cap(int cap, unsigned long long *hits, int reset)

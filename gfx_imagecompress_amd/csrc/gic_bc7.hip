@@ -156,18 +156,46 @@ __device__ __forceinline__ int anchor_of(int subsets, int part, int s)
 // Iteration cap: optQuantAnD_d's requantisation loop
 // `do ... while (!done && try_two--)` (amd_bc7_3dquant_vpc.cpp:1885,1986) never
 // resets try_two, so once it has run negative the reference loops until the
-// requantisation is stable -- forever on a cycling state.  The GPU stops such a
-// loop g_iter_cap rounds past the counter's exhaustion and counts the hit
-// (gic_iter_cap_hits); no tested input reaches it.
+// requantisation is stable -- forever on a cycling state.
+//  * The register quantisers of the integral kernels (bc7_quant.inc) stop such a
+//    loop g_iter_cap rounds past the counter's exhaustion, count the stop
+//    (g_iter_hits) and mark the block (BlockMeta.flags bit 3 + the call's
+//    re-run list, flag_capped).
+//  * run_chunks then re-runs the marked blocks through the general kernels,
+//    whose quantiser (opt_quant below) follows the reference's loop to its
+//    fixed point.  The loop's state is the index vector alone, so a revisited
+//    state proves the reference never returns: a Brent cycle check stops it
+//    there and counts the block in g_nonterm (no output of the reference
+//    exists for it).  kSafetyRounds bounds a pathological transient.
 __device__ int g_iter_cap = 4096;
 __device__ unsigned long long g_iter_hits = 0;
+__device__ unsigned long long g_nonterm = 0;
+constexpr int kSafetyRounds = 1 << 20;
 
-__device__ __forceinline__ bool iter_capped(int try_two, int cap)
-{
-    if (try_two >= -cap) return false;
-    atomicAdd(&g_iter_hits, 1ull);
-    return true;
-}
+// the reference's loop once try_two < 0: true = stop (cycle proven, or the
+// safety bound); state = the index vector as 4-bit nibbles
+struct CycleCheck {
+    uint64_t saved = 0;
+    int have = 0, pow = 1, lam = 0, rounds = 0;
+    __device__ __forceinline__ bool stop(uint64_t st)
+    {
+        if (have && st == saved) {
+            atomicAdd(&g_nonterm, 1ull);
+            return true;
+        }
+        if (++rounds > kSafetyRounds) {
+            atomicAdd(&g_iter_hits, 1ull);
+            return true;
+        }
+        if (!have || ++lam == pow) {
+            saved = st;
+            have = 1;
+            pow <<= 1;
+            lam = 0;
+        }
+        return false;
+    }
+};
 
 __device__ __forceinline__ int clog_of(int last)
 {
@@ -341,6 +369,7 @@ __device__ double opt_quant(const double data[][4], int n, int ncl, int *index, 
     for (int it = 0; it < 200; ++it) {
         if (it) {
             int done;
+            CycleCheck cyc;   // per requantisation loop: a state seen in an earlier loop proves nothing
             do {
                 double q = 0;
                 s = t = 0;
@@ -373,14 +402,15 @@ __device__ double opt_quant(const double data[][4], int n, int ncl, int *index, 
                     nidx[order[j]] = k;
                 }
                 done = 1;
+                uint64_t st = 0;
                 for (int j = 0; j < n; ++j) {
                     done = (done && (nidx[j] == index[j]));
                     index[j] = nidx[j];
+                    st |= (uint64_t)(nidx[j] & 15) << (4 * j);
                 }
                 // the reference's counter is never reset; past zero the loop
-                // runs until the requantisation is stable.  The cap keeps the
-                // GPU bounded and counts the hit (g_iter_hits).
-                if (iter_capped(try_two, g_iter_cap)) break;
+                // runs until the requantisation is stable (or, on a cycle, forever)
+                if (!done && try_two < 0 && cyc.stop(st)) break;
             } while (!done && try_two--);
             if (it == 1) {
                 for (int j = 0; j < n; ++j) snap[j] = index[j];
@@ -1311,9 +1341,25 @@ struct Params {
     // workspace slot b holds output block list[b] (a compacted list of the
     // blocks an earlier stage left unfinished), or first + b when list is null
     const uint32_t *list;
+    // H4: output ids of the blocks a capped register quantiser marked (the
+    // call's re-run list, h4_cap entries; *h4_cnt may exceed it = overflow)
+    uint32_t *h4_list;
+    uint32_t *h4_cnt;
+    uint32_t h4_cap;
+    int general;   // the re-run: every block through the general (f64, uncapped) kernels
 };
 
 __device__ __forceinline__ uint32_t out_block(const Params &p, uint32_t b) { return p.list ? p.list[b] : p.first + b; }
+
+// H4: a register quantiser of block b stopped at the iteration cap.  The block
+// is marked once (flags bit 3) and its output id appended to the re-run list.
+__device__ __forceinline__ void flag_capped(const Params &p, const Workspace &ws, uint32_t b)
+{
+    const uint32_t old = atomicOr(&ws.meta[b].flags, 8u);
+    if (old & 8u) return;
+    const uint32_t k = atomicAdd(p.h4_cnt, 1u);
+    if (k < p.h4_cap) p.h4_list[k] = out_block(p, b);
+}
 
 // BlockMeta.flags bit 2: the block met the error threshold in an earlier
 // stage (CompressBlock's mode-loop exit, :1440-1446)
@@ -1410,8 +1456,10 @@ __device__ void prep_block(const float inN[64], const Params &p, float *tex, Blo
     }
     // bit0: outside the implemented path (values outside [0,1] would need
     // optQuantTrace_d or index the reference's tables out of bounds);
-    // bit1: texels are integers, so every shaker error is an exact int32
-    meta.flags = (in_range ? 0u : 1u) | (integral ? 2u : 0u);
+    // bit1: texels are integers, so every shaker error is an exact int32 (the
+    // H4 re-run leaves it clear: the general kernels then take the block);
+    // bit3: a register quantiser hit the H4 cap (flag_capped)
+    meta.flags = (in_range ? 0u : 1u) | (integral && !p.general ? 2u : 0u);
 }
 
 __global__ void __launch_bounds__(256) k_prep_image(Geometry g, Params p, Workspace ws)
@@ -1559,7 +1607,9 @@ __global__ void __launch_bounds__(256, 3) k_quant_sub(Params p, Workspace ws)
         double err = 0.;
         uint64_t tidx = 0;
         if (spread) {
-            err = opt_quant_from<3>(px, SelPrefix{n}, pass == 0 ? 8 : 4, idx, mean, dir, qc);
+            int hit = 0;
+            err = opt_quant_from<3>(px, SelPrefix{n}, pass == 0 ? 8 : 4, idx, mean, dir, qc, &hit);
+            if (hit) flag_capped(p, ws, b);
             uint32_t m = mask;
 #pragma unroll
             for (int k = 0; k < 16; ++k)
@@ -1628,8 +1678,9 @@ __global__ void __launch_bounds__(256, 2) k_quant_reg(Params p, Workspace ws, in
 #pragma unroll
         for (int i = 0; i < 16; ++i) mask |= (((shape >> (2 * i)) & 3u) == (uint32_t)sub ? 1u : 0u) << i;
         if (!mask) continue;
-        int idx[16];
-        err += opt_quant_mask<DIM>(px, mask, ncl, idx);
+        int idx[16], hit = 0;
+        err += opt_quant_mask<DIM>(px, mask, ncl, idx, &hit);
+        if (hit) flag_capped(p, ws, b);
 #pragma unroll
         for (int i = 0; i < 16; ++i)
             if ((mask >> i) & 1u) tidx |= (uint64_t)(idx[i] & 15) << (4 * i);
@@ -2153,8 +2204,9 @@ __global__ void __launch_bounds__(256, 2) k_dual_quant_reg(Params p, Workspace w
         double qe = 0.;
         uint64_t ti = 0;
         if (spread) {
-            int idx[16];
-            qe = opt_quant_from<3>(px, SelPrefix{16}, ncl, idx, mean, dir, qc);
+            int idx[16], hit = 0;
+            qe = opt_quant_from<3>(px, SelPrefix{16}, ncl, idx, mean, dir, qc, &hit);
+            if (hit) flag_capped(p, ws, b);
 #pragma unroll
             for (int k = 0; k < 16; ++k) ti |= (uint64_t)(idx[k] & 15) << (4 * k);
         }
@@ -2732,7 +2784,32 @@ struct DeviceState {
     uint32_t *list[2] = {nullptr, nullptr};
     uint32_t list_cap = 0;
     uint32_t *count = nullptr;   // [4]
+    // H4 re-run list (output ids of capped blocks) and its count
+    uint32_t *h4_list = nullptr;
+    uint32_t h4_cap = 0;
+    uint32_t *h4_cnt = nullptr;
+    unsigned long long nonterm_seen = 0;   // g_nonterm at the end of the last call
 };
+
+// Caller holds g_state_lock.  Lanes are drained at the end of every call, so
+// the list can be replaced here.
+static hipError_t get_h4(DeviceState &st, uint32_t total)
+{
+    hipError_t e = hipSuccess;
+    if (!st.h4_cnt) {
+        e = hipMalloc(&st.h4_cnt, sizeof(uint32_t));
+        if (e != hipSuccess) return e;
+    }
+    const uint32_t want = total < (1u << 20) ? total : (1u << 20);   // more marked blocks: re-run the whole call
+    if (st.h4_cap >= want) return hipSuccess;
+    (void)hipFree(st.h4_list);
+    st.h4_list = nullptr;
+    st.h4_cap = 0;
+    e = hipMalloc(&st.h4_list, (size_t)want * sizeof(uint32_t));
+    if (e != hipSuccess) return e;
+    st.h4_cap = want;
+    return hipSuccess;
+}
 
 // Caller holds g_state_lock.  The lists are replaced only after both lanes
 // drained (earlier calls may still read them).
@@ -3023,7 +3100,14 @@ static void base_params(const gic_options &o, const DeviceState &st, double perf
     p.list = nullptr;
     p.first = 0;
     p.n = 0;
+    p.h4_list = st.h4_list;
+    p.h4_cnt = st.h4_cnt;
+    p.h4_cap = st.h4_cap;
+    p.general = 0;
 }
+
+// H4 report of the calling thread's last BC7 call (gic_last_h4_report)
+thread_local uint32_t t_h4_rerun = 0, t_h4_nonterm = 0;
 
 static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t total, const gic_options &o, void *dst,
                              double *err, hipStream_t s)
@@ -3048,6 +3132,11 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
         e = get_trace(*st);
         if (e != hipSuccess) return e;
     }
+    e = get_h4(*st, total);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(st->h4_cnt, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    t_h4_rerun = t_h4_nonterm = 0;
     Params base;
     base_params(o, *st, perf, base);
     // err_thr > 0 (quality < 0.25): CompressBlock stops visiting modes once a
@@ -3082,6 +3171,20 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
         for (int k : {0, 2, 3})
             if (valid_modes & (1u << order[k])) stages[nstages++] = k;
     stages[nstages++] = -1;   // the search itself
+    // the search over one chunk (the modes in one launch sequence, or staged)
+    auto search = [&](Params p, const Workspace &ws, hipStream_t s, bool integral) {
+        int resume = 0;
+        for (int k = 0; k < (staged ? 8 : 1); ++k) {
+            p.stage_mask = staged ? (1u << order[k]) : 0xFFu;
+            const bool last = !staged || k == 7;
+            const bool skip = staged && !(valid_modes & p.stage_mask);
+            if (skip && !last) continue;
+            if (!skip) run_modes(p, ws, st->sp, s, integral);
+            hipLaunchKernelGGL(k_select, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, p, ws, (uint4 *)dst, err,
+                               staged ? k : 0, staged ? k + 1 : 8, resume);
+            resume = 1;
+        }
+    };
     const uint32_t *cur = nullptr;
     uint32_t cur_n = total;
     uint32_t ci = 0;
@@ -3115,17 +3218,7 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
                 hipLaunchKernelGGL(k_compact, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, pp, ws, out,
                                    st->count + si);
             } else {
-                int resume = 0;
-                for (int k = 0; k < (staged ? 8 : 1); ++k) {
-                    p.stage_mask = staged ? (1u << order[k]) : 0xFFu;
-                    const bool last = !staged || k == 7;
-                    const bool skip = staged && !(valid_modes & p.stage_mask);
-                    if (skip && !last) continue;
-                    if (!skip) run_modes(p, ws, st->sp, s, g != nullptr);
-                    hipLaunchKernelGGL(k_select, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, p, ws, (uint4 *)dst, err,
-                                       staged ? k : 0, staged ? k + 1 : 8, resume);
-                    resume = 1;
-                }
+                search(p, ws, s, g != nullptr);
             }
             e = hipGetLastError();
             if (e != hipSuccess) return e;
@@ -3141,6 +3234,44 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
             cur = out;
             cur_n = n_next;
         }
+    }
+    // H4: blocks whose register quantiser stopped at the iteration cap are
+    // encoded again through the general kernels (uncapped, cycle-checked
+    // quantiser), so their output is the reference's.  Deciding needs the
+    // marked count on the host: a BC7 call returns with its work complete.
+    for (int k = 0; k < nsets && e == hipSuccess; ++k) e = hipStreamSynchronize(st->lane[k]);
+    uint32_t nh = 0;
+    if (e == hipSuccess) e = hipMemcpy(&nh, st->h4_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return e;
+    if (nh > 0) {
+        const uint32_t *rl = nh <= st->h4_cap ? st->h4_list : nullptr;   // overflow: the whole call
+        const uint32_t rn = rl ? nh : total;
+        for (uint32_t first = 0; first < rn; first += chunk) {
+            const Workspace &ws = st->ws[0];
+            s = st->lane[0];
+            Params p = base;
+            p.general = 1;
+            p.first = first;
+            p.n = (rn - first) < chunk ? (rn - first) : chunk;
+            p.list = rl ? rl + first : nullptr;
+            if (g)
+                hipLaunchKernelGGL(k_prep_image, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, *g, p, ws);
+            else
+                hipLaunchKernelGGL(k_prep_f32, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, blocks, p, ws);
+            search(p, ws, s, false);
+            e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        e = hipStreamSynchronize(st->lane[0]);
+        if (e != hipSuccess) return e;
+        t_h4_rerun = rn;
+    }
+    {
+        unsigned long long nt = 0;
+        e = hipMemcpyFromSymbol(&nt, HIP_SYMBOL(g_nonterm), sizeof(nt));
+        if (e != hipSuccess) return e;
+        t_h4_nonterm = (uint32_t)(nt - st->nonterm_seen);
+        st->nonterm_seen = nt;
     }
     {   // join: the caller's stream waits for the lanes
         for (int k = 0; k < nsets && e == hipSuccess; ++k) {
@@ -3211,6 +3342,26 @@ hipError_t launch_bc7_blocks(const float *blocks, uint32_t n, const gic_options 
                              hipStream_t s)
 {
     return bc7::run_chunks(nullptr, blocks, n, o, dst, err, s);
+}
+
+hipError_t bc7_nonterm(unsigned long long *n, int reset)
+{
+    std::lock_guard<std::mutex> lk(bc7::g_state_lock);
+    hipError_t e = hipMemcpyFromSymbol(n, HIP_SYMBOL(bc7::g_nonterm), sizeof(*n));
+    if (e == hipSuccess && reset) {
+        const unsigned long long z = 0;
+        e = hipMemcpyToSymbol(HIP_SYMBOL(bc7::g_nonterm), &z, sizeof(z));
+        int dev = 0;
+        if (e == hipSuccess) e = hipGetDevice(&dev);
+        if (e == hipSuccess && dev >= 0 && dev < 64) bc7::g_states[dev].nonterm_seen = 0;
+    }
+    return e;
+}
+
+void bc7_last_h4(uint32_t *rerun, uint32_t *nonterm)
+{
+    if (rerun) *rerun = bc7::t_h4_rerun;
+    if (nonterm) *nonterm = bc7::t_h4_nonterm;
 }
 
 }  // namespace gic

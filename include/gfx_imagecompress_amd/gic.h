@@ -186,18 +186,34 @@ int gic_last_hip_error(void);
  * a failed one writes a zero block, prints to stderr and sets this status. */
 int gic_block_last_status(void);
 
-/* Iteration caps.  The reference's BC7 and BC6H quantisers
- * (optQuantAnD_d, amd_bc7_3dquant_vpc.cpp:1885-1986; optQuantAnD_f,
+/* Unbounded quantiser loops.  The reference's BC7 and BC6H
+ * quantisers (optQuantAnD_d, amd_bc7_3dquant_vpc.cpp:1885-1986; optQuantAnD_f,
  * amd_hdr_encode.cpp:1427-1601) requantise in `do ... while (!done && try_two--)`
  * with a counter that is never reset: once it has run negative the loop runs
- * until the requantisation is stable, forever on a cycling state.  The GPU
- * stops such a loop `cap` rounds past the counter's exhaustion (default 4096)
- * and counts each stop on the current device; a block with a hit differs from
- * the reference, which would not have returned.
- *   gic_iter_cap_hits: the count since the last reset (synchronises the device);
- *   gic_set_iter_cap: the cap (< 0 restores 4096; a small cap is a test hook). */
+ * until the requantisation is stable, forever on a cycling state.  The loop's
+ * state is the index vector alone, so a revisited state proves the reference
+ * never returns.
+ *  - BC7: the fast (register) quantisers stop a loop `cap` rounds past the
+ *    counter's exhaustion (default 4096), count the stop and mark the block;
+ *    every marked block is then encoded again through the general kernels,
+ *    whose quantiser runs the reference's loop to its fixed point (a BC7 call
+ *    returns with its device work complete for that reason).  The result is the
+ *    reference's on every block where the reference returns; a loop proven
+ *    cyclic stops and is counted as non-terminating.
+ *  - BC6H: each loop stops at a proven cycle (non-terminating) or after `cap`
+ *    rounds past the exhaustion within that loop (counted as a cap stop); the
+ *    oracle (oracle/orc_bc6h.c) applies the same stops.
+ *   gic_iter_cap_hits: cap stops since the last reset on the current device
+ *     (synchronises the device); a BC7 stop means a re-run, not a wrong block;
+ *   gic_set_iter_cap: the cap (< 0 restores 4096; a small cap is a test hook);
+ *   gic_nonterminating_loops: loops proven cyclic since the last reset (the
+ *     reference would never have returned on those blocks);
+ *   gic_last_h4_report: this thread's last BC7 call -- blocks re-run after a
+ *     cap stop, and loops proven cyclic during the call. */
 int gic_iter_cap_hits(unsigned long long *hits, int reset);
 int gic_set_iter_cap(int cap);
+int gic_nonterminating_loops(unsigned long long *loops, int reset);
+int gic_last_h4_report(uint32_t *rerun_blocks, uint32_t *nonterminating_loops);
 
 /* Library version string. */
 const char *gic_version(void);

@@ -97,6 +97,11 @@ int orc_encode_image_bc7_perf(const uint8_t *src, uint32_t width, uint32_t heigh
  * Parity-unpinned: Math_Float2Half is taken as IEEE binary16 RNE (orc_bc6h.c). */
 float orc_bc6h_block(const float in[64], int is_signed, uint8_t out[16]);
 int orc_encode_bc6h_blocks(const float *blocks, int n, int is_signed, int threads, uint8_t *out, float *err);
+/* H4 stops of optQuantAnD_f's requantisation loop: the per-loop cap (rounds past
+ * try_two's exhaustion, < 0 = 4096) and the cumulative stop counts (proven
+ * cycles, cap hits) */
+void orc_bc6h_set_cap(int cap);
+void orc_bc6h_h4_counts(unsigned long long *nonterm, unsigned long long *capped);
 /* test hooks: FindBestPattern of one pattern (-1 = one region), the half
  * conversion, the BPTC anchors, eigenVector_d's squaring count */
 float orc_bc6h_pattern(const float in[64], int is_signed, int shape, float fep[12], int idx[32], int cnt[2]);

@@ -260,10 +260,21 @@ static void shell_f(const float *v_, int k, int n, int *idx)
     for (int i = 0; i < n; ++i) idx[i] -= mi;
 }
 
-/* the bound on the requantisation loop once try_two has run negative (the
- * reference's `while (!done && try_two--)` then loops until a fixed point);
- * the GPU uses the same bound */
-#define BC6H_TRY_TWO_FLOOR (-4096)
+/* Once try_two has run negative the reference's `while (!done && try_two--)`
+ * loops until a fixed point -- forever on a cycling state.  The loop's state is
+ * the index vector alone, so a revisited state proves non-termination: a Brent
+ * cycle check stops the loop there (the reference never returns for such a
+ * block), and a loop still running g_cap rounds past the exhaustion within
+ * one loop stops too.  The GPU (gic_bc6h.hip opt_quant_f) applies the same two
+ * stops in the same order, so both agree on every block. */
+static int g_cap = 4096;
+static unsigned long long g_nonterm_loops, g_cap_loops;
+void orc_bc6h_set_cap(int cap) { g_cap = cap < 0 ? 4096 : cap; }
+void orc_bc6h_h4_counts(unsigned long long *nonterm, unsigned long long *capped)
+{
+    if (nonterm) *nonterm = __atomic_load_n(&g_nonterm_loops, __ATOMIC_RELAXED);
+    if (capped) *capped = __atomic_load_n(&g_cap_loops, __ATOMIC_RELAXED);
+}
 
 /* optQuantAnD_f, amd_hdr_encode.cpp:1427-1601 (dimension 3, quality 1.0) */
 static float opt_quant_f(float data[][4], int n, int ncl, int *index, float out[][4], float dir[4])
@@ -298,6 +309,8 @@ static float opt_quant_f(float data[][4], int n, int ncl, int *index, float out[
     for (int it = 0; it < max_try; ++it) {
         if (it) {
             int done;
+            uint64_t cyc_saved = 0;
+            int cyc_have = 0, cyc_pow = 1, cyc_lam = 0, cyc_rounds = 0;
             do {
                 float q = 0;
                 s = t = 0;
@@ -334,11 +347,28 @@ static float opt_quant_f(float data[][4], int n, int ncl, int *index, float out[
                     nidx[order[j]] = k;
                 }
                 done = 1;
+                uint64_t st = 0;
                 for (int j = 0; j < n; ++j) {
                     done = (done && (nidx[j] == index[j]));
                     index[j] = nidx[j];
+                    st |= (uint64_t)(nidx[j] & 15) << (4 * j);
                 }
-                if (try_two < BC6H_TRY_TWO_FLOOR) break;
+                if (!done && try_two < 0) {
+                    if (cyc_have && st == cyc_saved) {   /* a cycle: the reference never returns */
+                        __atomic_fetch_add(&g_nonterm_loops, 1, __ATOMIC_RELAXED);
+                        break;
+                    }
+                    if (++cyc_rounds > g_cap) {
+                        __atomic_fetch_add(&g_cap_loops, 1, __ATOMIC_RELAXED);
+                        break;
+                    }
+                    if (!cyc_have || ++cyc_lam == cyc_pow) {
+                        cyc_saved = st;
+                        cyc_have = 1;
+                        cyc_pow <<= 1;
+                        cyc_lam = 0;
+                    }
+                }
             } while (!done && try_two--);
             if (it == 1) {
                 for (int j = 0; j < n; ++j) snap[j] = index[j];

@@ -6,7 +6,8 @@
  * block columns) and ReadNxNBlockF / ReadNxNSingleBlockF edge clamping
  * (src/block_utils.cpp:7-41, :116-144).  The UNORM8 -> float conversion
  * (Image_GetPixelAtF in the un-vendored gfx_image) is restated as v/255.0f.
- * A pthread pool over block rows provides the multi-core CPU baseline.
+ * A pthread pool over block rows (BC7: pieces of 16 blocks of a row) provides the
+ * multi-core CPU baseline.
  */
 #include "bcn_oracle.h"
 
@@ -61,16 +62,19 @@ typedef struct {
     int bc7_ranks;       /* shake-rank cap (0 = reference) */
     int enc_fast, enc_perceptual;   /* bc7enc16 (fmt 8) settings */
     float bc7_perf;      /* BC7BlockEncoder performance (image API: 1.0) */
-    int next;            /* next job (slice*nrows + row) */
+    int next;            /* next job ((slice*nrows + row)*row_jobs + column piece) */
     int njobs;
+    uint32_t row_jobs;   /* jobs per block row: 1, or pieces of kBc7Piece blocks for BC7 */
     pthread_mutex_t lock;
 } job_t;
+
+enum { kBc7Piece = 16 };   /* BC7 job size in blocks */
 
 static size_t block_bytes(int fmt) { return (fmt == 1 || fmt == 4) ? 8 : 16; }
 static int g_enc_fast, g_enc_perceptual;   /* set by orc_encode_image_bc7enc_rows before the pool runs */
 static __thread float t_bc7_perf = 1.0f;   /* set by orc_encode_image_bc7_perf for its own call */
 
-static void encode_row(job_t *j, uint32_t slice, uint32_t brow)
+static void encode_row(job_t *j, uint32_t slice, uint32_t brow, uint32_t bx0, uint32_t bx1)
 {
     const size_t slice_px = (size_t)j->width * j->height * j->channels;
     const uint8_t *img = j->src + slice_px * slice;
@@ -78,7 +82,7 @@ static void encode_row(job_t *j, uint32_t slice, uint32_t brow)
     const int has_alpha = j->channels > 3;
     /* output is the shard's own contiguous region: rows [row0,row0+nrows) of every slice */
     const size_t out_row = ((size_t)slice * j->nrows + (brow - j->row0)) * j->bx_count;
-    for (uint32_t bx = 0; bx < j->bx_count; ++bx) {
+    for (uint32_t bx = bx0; bx < bx1; ++bx) {
         float blk[64], ch[16];
         uint8_t *o = j->dst + (out_row + bx) * bb;
         double e = 0.0;
@@ -136,7 +140,10 @@ static void *worker(void *arg)
         int k = j->next++;
         pthread_mutex_unlock(&j->lock);
         if (k >= j->njobs) break;
-        encode_row(j, (uint32_t)(k / (int)j->nrows), j->row0 + (uint32_t)(k % (int)j->nrows));
+        const uint32_t piece = (uint32_t)k % j->row_jobs, rk = (uint32_t)k / j->row_jobs;
+        const uint32_t w = (j->bx_count + j->row_jobs - 1) / j->row_jobs;
+        const uint32_t bx0 = piece * w, bx1 = bx0 + w < j->bx_count ? bx0 + w : j->bx_count;
+        if (bx0 < bx1) encode_row(j, rk / j->nrows, j->row0 + rk % j->nrows, bx0, bx1);
     }
     return NULL;
 }
@@ -169,7 +176,10 @@ static int encode_image(int fmt, const uint8_t *src, uint32_t width, uint32_t he
     if (j.row0 + j.nrows > j.by_count) return -1;
     j.dst = dst;
     j.err = block_err;
-    j.njobs = (int)(j.nrows * slices);
+    /* BC7 costs ~10 ms per block on one core: a block row is split into pieces of
+     * kBc7Piece blocks so that a sample of a few rows still keeps every thread busy */
+    j.row_jobs = fmt == 7 ? (j.bx_count + kBc7Piece - 1) / kBc7Piece : 1;
+    j.njobs = (int)(j.nrows * slices * j.row_jobs);
     pthread_mutex_init(&j.lock, NULL);
     if (threads <= 1) {
         worker(&j);

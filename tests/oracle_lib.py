@@ -82,6 +82,10 @@ def lib() -> ctypes.CDLL:
         _lib.orc_encode_bc6h_blocks.restype = ctypes.c_int
         _lib.orc_bc6h_block.argtypes = [vp, ctypes.c_int, vp]
         _lib.orc_bc6h_block.restype = ctypes.c_float
+        _lib.orc_bc6h_set_cap.argtypes = [ctypes.c_int]
+        _lib.orc_bc6h_set_cap.restype = None
+        _lib.orc_bc6h_h4_counts.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong)]
+        _lib.orc_bc6h_h4_counts.restype = None
         _lib.orc_float_to_half.argtypes = [ctypes.c_float]
         _lib.orc_float_to_half.restype = ctypes.c_uint16
         _lib.orc_bc6h_anchor.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
@@ -245,6 +249,18 @@ def bc6h_blocks(blocks: np.ndarray, signed: bool = False, threads: int = 0):
     threads = threads or min(os.cpu_count() or 1, 16)
     lib().orc_encode_bc6h_blocks(b.ctypes.data, b.shape[0], int(signed), threads, out.ctypes.data, err.ctypes.data)
     return out, err
+
+
+def bc6h_set_cap(cap: int) -> None:
+    """The oracle's per-loop H4 cap of optQuantAnD_f (< 0 = the default 4096)."""
+    lib().orc_bc6h_set_cap(int(cap))
+
+
+def bc6h_h4_counts() -> tuple[int, int]:
+    """Cumulative (proven cycles, cap stops) of the oracle's BC6H quantiser loops."""
+    a, b = ctypes.c_ulonglong(0), ctypes.c_ulonglong(0)
+    lib().orc_bc6h_h4_counts(ctypes.byref(a), ctypes.byref(b))
+    return int(a.value), int(b.value)
 
 
 def bc7_decode(blocks: np.ndarray) -> np.ndarray:

@@ -164,6 +164,66 @@ def test_two_rank_shards_reassemble_to_single_process_encode():
             assert n0 == 3 * 9 * 2 * bb and n1 == 2 * 9 * 2 * bb
 
 
+def _split_worker(rank, world, port, q):
+    """bench.py's 8K split: rank r encodes block rows shard_rows(BY, N, r) of the
+    ONE texture into its RootGather buffer, one gather to rank 0 per step."""
+    try:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench
+        import oracle_lib
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        res = []
+        for fmt, size in ((1, 64), (1, 52), (5, 40)):
+            ch = 4 if fmt == 1 else 2
+            img = synth.g1(size, size)[..., :ch] if fmt == 1 else synth.noise_rgba(size, size, seed=5)[..., :2]
+            img = np.ascontiguousarray(img)
+            by = bx = (size + 3) // 4
+            split = bench.Split(by, world, rank, weak=False)
+            g = bench.RootGather(split, bx, 8 if fmt == 1 else 16, "cpu")
+            out = oracle_lib.encode_image(fmt, img, bc4_channel=0, first_row=split.first, num_rows=split.rows,
+                                          threads=2).reshape(-1)
+            g.local[: out.size] = torch.from_numpy(out)
+            for _ in range(2):      # two timed steps gather twice: idempotent
+                g()
+            res.append((fmt, size, split.first, split.rows, None if rank else g.image_host().tobytes()))
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, res))
+    except Exception as e:   # pragma: no cover
+        q.put((rank, repr(e)))
+
+
+def test_bench_8k_split_reassembles_one_image():
+    """The strong-scaling split of bench.py's 8K workload (reduced sizes, one of
+    them not a multiple of the rank count): the gathered image on rank 0 equals
+    the single-process encode byte for byte; rank 1 receives nothing."""
+    import oracle_lib
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_split_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert not isinstance(got[r], str), got[r]
+    for i, (fmt, size) in enumerate(((1, 64), (1, 52), (5, 40))):
+        ch = 4 if fmt == 1 else 2
+        img = synth.g1(size, size)[..., :ch] if fmt == 1 else synth.noise_rgba(size, size, seed=5)[..., :2]
+        ref = oracle_lib.encode_image(fmt, np.ascontiguousarray(img), bc4_channel=0, threads=2).tobytes()
+        by = (size + 3) // 4
+        f0, s0, first0, rows0, img0 = got[0][i]
+        f1, s1, first1, rows1, img1 = got[1][i]
+        assert (first0, rows0, first1, rows1) == (0, (by + 1) // 2, (by + 1) // 2, by // 2)
+        assert img0 == ref and img1 is None
+
+
 def test_bench_gpus_flag_launches_ranks(monkeypatch):
     """bench.py --gpus N outside torchrun starts N ranks as a child
     torch.distributed.run (no exec, before any GPU call); under torchrun a

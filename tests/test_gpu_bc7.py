@@ -286,32 +286,54 @@ def test_bc7_dual_index_regression_blocks(gpu, mask):
 def test_iteration_cap_hits_are_counted(gpu):
     """the reference's requantisation loop (optQuantAnD_d,
     amd_bc7_3dquant_vpc.cpp:1885-1986; optQuantAnD_f for BC6H) never resets its
-    counter, so past its exhaustion it runs until the state is stable.  The GPU
-    stops such a loop at a cap and counts the stop (gic_iter_cap_hits).  At the
-    default cap a G1 band and an HDR image reach it nowhere (the output equals
-    the oracle's); with the cap at 0 (every loop stopped as soon as the
-    reference's counter runs out -- blocks that need more requantisation
-    passes than its budget of 50) the counter reports the stops."""
+    counter, so past its exhaustion it runs until the state is stable.  At the
+    default cap a G1 band and an HDR image reach no cap (the output equals the
+    oracle's).  With the cap at 0 every BC7 register-quantiser loop stops as
+    soon as the reference's counter runs out (blocks that need more
+    requantisation passes than its budget of 50): the stops are counted, their
+    blocks marked and encoded again through the uncapped general path in the
+    same call -- so the output still equals the oracle on every block, and
+    gic_last_h4_report names the re-run blocks.  BC6H applies the cap per loop
+    and so does its oracle: at cap 0 and cap 3 both stop the same loops and
+    the blocks stay bit-identical (the 4000-round fast-forward is exact under
+    the cap)."""
     import torch
     img = synth.g1(256, 64)
     hdr = synth.hdr_rgba(256, 256, seed=3)
     src = torch.from_numpy(hdr.reshape(-1).copy()).cuda()
     dst = torch.zeros(64 * 64 * 16, dtype=torch.uint8, device="cuda")
+    ref7 = oracle_lib.encode_image_bc7(img, first_row=0, num_rows=4)
+    blocks = hdr.reshape(64, 4, 64, 4, 4).transpose(0, 2, 1, 3, 4).reshape(-1, 64)
     gic.iter_cap_hits(reset=True)
     out = gpu_encode(7, img)
     assert gic.iter_cap_hits(reset=True) == 0
-    assert np.array_equal(out[:64], oracle_lib.encode_image_bc7(img, first_row=0, num_rows=1))
+    assert gic.last_h4_report() == (0, 0)
+    assert np.array_equal(out[:256], ref7)
     gic.encode_device_src(gic.FMT_BC6H, gic.SRC_FLOAT32, src, 256, 256, 1, 4, dst)
     assert gic.iter_cap_hits(reset=True) == 0
+    ref6, _ = oracle_lib.bc6h_blocks(blocks)
+    assert np.array_equal(dst.cpu().numpy().reshape(-1, 16), ref6)
+    hits6 = {}
     gic.set_iter_cap(0)
     try:
-        gpu_encode(7, img)
+        out0 = gpu_encode(7, img)
         hits7 = gic.iter_cap_hits(reset=True)
-        gic.encode_device_src(gic.FMT_BC6H, gic.SRC_FLOAT32, src, 256, 256, 1, 4, dst)
-        hits6 = gic.iter_cap_hits(reset=True)
+        rerun, nonterm = gic.last_h4_report()
+        for cap in (0, 3):
+            gic.set_iter_cap(cap)
+            oracle_lib.bc6h_set_cap(cap)
+            gic.encode_device_src(gic.FMT_BC6H, gic.SRC_FLOAT32, src, 256, 256, 1, 4, dst)
+            hits6[cap] = gic.iter_cap_hits(reset=True)
+            ref_c, _ = oracle_lib.bc6h_blocks(blocks)
+            got = dst.cpu().numpy().reshape(-1, 16)
+            assert np.array_equal(got, ref_c), (cap, int((got != ref_c).any(axis=1).sum()))
     finally:
         gic.set_iter_cap(-1)
-    print(f"\ncap 0: {hits7} BC7 and {hits6} BC6H quantiser loops stopped")
-    assert hits7 > 0 and hits6 > 0
+        oracle_lib.bc6h_set_cap(-1)
+    print(f"\ncap 0: {hits7} BC7 loops stopped, {rerun} blocks re-run, {nonterm} cyclic; BC6H stops {hits6}")
+    assert hits7 > 0 and rerun > 0 and nonterm == 0 and hits6[0] > 0
+    assert np.array_equal(out0[:256], ref7)        # the re-run blocks are the reference's
+    assert np.array_equal(out0, out)
     gpu_encode(7, img[:8])
     assert gic.iter_cap_hits(reset=True) == 0   # the default cap is back
+    assert gic.last_h4_report() == (0, 0)
