@@ -23,7 +23,7 @@ __all__ = [
     "GicError", "Options", "FMT_BC1", "FMT_BC2", "FMT_BC3", "FMT_BC4", "FMT_BC5", "FMT_BC6H", "FMT_BC6H_SF",
     "FMT_BC7", "FMT_BC7ENC16", "compress_bc6h",
     "library", "encode_blocks_u8", "compress_bc7_fast", "iter_cap_hits", "set_iter_cap", "nonterminating_loops",
-    "last_h4_report",
+    "last_h4_report", "encode_multi", "multi_split",
     "block_bytes", "blocks_shape", "encode_device", "encode_device_src", "encode_blocks_f32", "decode_device", "compress_bc1", "compress_bc2",
     "compress_bc3", "compress_bc4", "compress_bc5", "compress_bc7", "LIB_PATH",
 ]
@@ -127,6 +127,11 @@ class Options:
         return Options(bc7enc_perceptual=perceptual, bc7enc_uber_level=0 if fast else 4)
 
 
+class _MultiReport(ctypes.Structure):
+    _fields_ = [("ranks", ctypes.c_int), ("rccl", ctypes.c_int), ("encode_ms_max", ctypes.c_double),
+                ("gather_ms", ctypes.c_double), ("gathered_bytes", ctypes.c_uint64)]
+
+
 _lib = None
 
 
@@ -175,6 +180,16 @@ def library() -> ctypes.CDLL:
     lib.gic_nonterminating_loops.restype = ctypes.c_int
     lib.gic_last_h4_report.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
     lib.gic_last_h4_report.restype = ctypes.c_int
+    lib.gic_encode_multi.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                     ctypes.c_uint32, ctypes.c_uint32, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int,
+                                     ctypes.POINTER(ctypes.c_int), ctypes.c_void_p, ctypes.c_uint32]
+    lib.gic_encode_multi.restype = ctypes.c_int
+    lib.gic_multi_last_report.argtypes = [ctypes.POINTER(_MultiReport)]
+    lib.gic_multi_last_report.restype = ctypes.c_int
+    lib.gic_multi_release.restype = ctypes.c_int
+    lib.gic_multi_split.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+                                    ctypes.POINTER(ctypes.c_uint64)]
+    lib.gic_multi_split.restype = ctypes.c_int
     _lib = lib
     return lib
 
@@ -216,6 +231,39 @@ def last_h4_report() -> tuple[int, int]:
     last BC7 call (gic_last_h4_report)."""
     a, b = ctypes.c_uint32(0), ctypes.c_uint32(0)
     _check(library().gic_last_h4_report(ctypes.byref(a), ctypes.byref(b)))
+    return int(a.value), int(b.value)
+
+
+def encode_multi(fmt: int, image, devices, dst, options: Options | None = None, src_type: int = 0,
+                 peer_copy: bool = False) -> dict:
+    """gic_encode_multi: the block rows of a host image stack (numpy (S,H,W,C)
+    or (H,W,C); uint8, int8 or float32 per ``src_type``) split over ``devices``
+    of this process, one gather into ``dst`` (a uint8 tensor on devices[0]).
+    Returns the call's report (ranks, rccl, encode_ms_max, gather_ms,
+    gathered_bytes)."""
+    import numpy as np
+    a = np.ascontiguousarray(image)
+    if a.ndim == 3:
+        a = a[None]
+    s, h, w, c = a.shape
+    bx, by = blocks_shape(w, h)
+    if not dst.is_cuda or dst.numel() * dst.element_size() < bx * by * s * block_bytes(fmt):
+        raise GicError("dst must be a device tensor holding the whole image's blocks")
+    devs = (ctypes.c_int * len(devices))(*devices)
+    opts = (options or Options()).to_c()
+    rc = library().gic_encode_multi(fmt, src_type, a.ctypes.data, w, h, s, c, w * c * a.itemsize, ctypes.byref(opts),
+                                    len(devices), devs, dst.data_ptr(), 1 if peer_copy else 0)
+    _check(rc)
+    r = _MultiReport()
+    _check(library().gic_multi_last_report(ctypes.byref(r)))
+    return {"ranks": r.ranks, "rccl": bool(r.rccl), "encode_ms_max": r.encode_ms_max, "gather_ms": r.gather_ms,
+            "gathered_bytes": int(r.gathered_bytes)}
+
+
+def multi_split(rows_total: int, ndev: int, i: int) -> tuple[int, int]:
+    """(first slice-major block row, rows) of device i in gic_encode_multi."""
+    a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    _check(library().gic_multi_split(rows_total, ndev, i, ctypes.byref(a), ctypes.byref(b)))
     return int(a.value), int(b.value)
 
 

@@ -562,6 +562,26 @@ struct DeviceScratch {
 };
 static thread_local DeviceScratch t_scratch;
 
+// GIC_DEVICES: a comma-separated device list for the image-level entry points
+static std::vector<int> env_devices()
+{
+    std::vector<int> out;
+    const char *e = getenv("GIC_DEVICES");
+    if (!e) return out;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) return {};
+    for (const char *p = e; *p;) {
+        char *end = nullptr;
+        const long v = strtol(p, &end, 10);
+        if (end == p) break;
+        if (v < 0 || v >= count) return {};
+        out.push_back((int)v);
+        p = *end == ',' ? end + 1 : end;
+        if (*end && *end != ',') break;
+    }
+    return out;
+}
+
 // Host-image driver shared by the image-level wrappers: uploads the source,
 // encodes in chunks of block rows, reports progress per block row exactly as
 // the reference loops do (amd_bc1_compressor.cpp:64-68), downloads blocks.
@@ -584,6 +604,28 @@ static Image_ImageHeader const *encode_host_image(Image_ImageHeader const *src, 
     const size_t src_bytes = pitch * src->height * src->slices;
     const size_t bb = gic_block_bytes(fmt);
     const size_t dst_bytes = (size_t)bx * by * src->slices * bb;
+    // GIC_DEVICES="0,1,..." (more than one device) and no progress callback: the
+    // block rows go over the listed devices with one gather (gic_encode_multi)
+    std::vector<int> devs;
+    if (!cb) devs = env_devices();
+    if (devs.size() > 1) {
+        int cur = 0;
+        bool ok = hipGetDevice(&cur) == hipSuccess && hipSetDevice(devs[0]) == hipSuccess;
+        uint8_t *d = nullptr;
+        ok = ok && hipMalloc((void **)&d, dst_bytes) == hipSuccess;
+        ok = ok && gic_encode_multi(fmt, st, src->data, src->width, src->height, src->slices, ch, pitch, &o,
+                                    (int)devs.size(), devs.data(), d, 0) == GIC_OK;
+        ok = ok && hipSetDevice(devs[0]) == hipSuccess &&
+             hipMemcpy(dst->data, d, dst_bytes, hipMemcpyDeviceToHost) == hipSuccess;
+        if (d) (void)hipFree(d);
+        (void)hipSetDevice(cur);
+        if (!ok) {
+            fprintf(stderr, "gfx_imagecompress_amd: multi-GPU encode failed\n");
+            Image_Destroy(dst);
+            return nullptr;
+        }
+        return dst;
+    }
     DeviceScratch &s = t_scratch;
     bool ok = s.reserve(src_bytes, dst_bytes) &&
               hipMemcpyAsync(s.src, src->data, src_bytes, hipMemcpyHostToDevice, s.stream) == hipSuccess;

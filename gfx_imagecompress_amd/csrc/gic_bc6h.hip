@@ -1511,12 +1511,12 @@ constexpr uint32_t kChunk = 1u << 16;
 
 static hipError_t upload_tables()
 {
-    static bool done = false;   // guarded by the caller's lock
-    static int dev_done = -1;
+    static bool done[64] = {};   // per device, guarded by the caller's lock
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    if (done && dev_done == dev) return hipSuccess;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    if (done[dev]) return hipSuccess;
     uint32_t shp[32];
     uint8_t anc[32];
     for (int s = 0; s < 32; ++s) {
@@ -1525,10 +1525,7 @@ static hipError_t upload_tables()
     }
     e = hipMemcpyToSymbol(HIP_SYMBOL(dShape), shp, sizeof(shp));
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dAnchor), anc, sizeof(anc));
-    if (e == hipSuccess) {
-        done = true;
-        dev_done = dev;
-    }
+    if (e == hipSuccess) done[dev] = true;
     return e;
 }
 

@@ -2791,7 +2791,7 @@ struct DeviceState {
     unsigned long long nonterm_seen = 0;   // g_nonterm at the end of the last call
 };
 
-// Caller holds g_state_lock.  Lanes are drained at the end of every call, so
+// Caller holds its device's lock.  Lanes are drained at the end of every call, so
 // the list can be replaced here.
 static hipError_t get_h4(DeviceState &st, uint32_t total)
 {
@@ -2811,7 +2811,7 @@ static hipError_t get_h4(DeviceState &st, uint32_t total)
     return hipSuccess;
 }
 
-// Caller holds g_state_lock.  The lists are replaced only after both lanes
+// Caller holds its device's lock.  The lists are replaced only after both lanes
 // drained (earlier calls may still read them).
 static hipError_t get_lists(DeviceState &st, uint32_t total)
 {
@@ -2838,7 +2838,7 @@ static hipError_t get_lists(DeviceState &st, uint32_t total)
     return hipSuccess;
 }
 
-// Caller holds g_state_lock.
+// Caller holds its device's lock.
 static hipError_t get_trace(DeviceState &st)
 {
     if (st.trace.kc) return hipSuccess;
@@ -2868,24 +2868,55 @@ static hipError_t get_trace(DeviceState &st)
     return hipSuccess;
 }
 
-static std::mutex g_state_lock;
+// One lock per device: a call holds its device's lock while it enqueues its
+// passes (and, for the H4 decision, until they complete), so calls on one
+// device are serialised while devices driven from different host threads
+// (gic_encode_multi) run concurrently.
+static std::mutex g_dev_lock[64];
 static DeviceState g_states[64];
+
+static hipError_t current_device(int &dev)
+{
+    const hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    return (dev < 0 || dev >= 64) ? hipErrorInvalidDevice : hipSuccess;
+}
+
+// the host-built tables shared by every device (built once)
+struct HostTables {
+    std::vector<SpEntry> sp;
+    std::vector<uint32_t> prob, minpart, pairs;
+    std::vector<uint16_t> tsub;
+    int nu = 0, nm = 0;
+};
+static const HostTables &host_tables()
+{
+    static HostTables t;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        build_sp_table(t.sp);
+        t.nu = build_subset_problems(t.prob, t.minpart, t.tsub);
+        t.nm = build_subset_masks(t.prob, t.pairs);
+        g_nu = t.nu;
+        g_nm = t.nm;
+    });
+    return t;
+}
 
 static size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
 
-// Caller holds g_state_lock.  Tables are published (st.sp set) only after
+// Caller holds its device's lock.  Tables are published (st.sp set) only after
 // every upload succeeded; a workspace is reallocated only after its lane has
 // drained, since earlier calls may still be using it.
 static hipError_t get_state(uint32_t chunk, int nsets, DeviceState *&out)
 {
     int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
+    hipError_t e = current_device(dev);
     if (e != hipSuccess) return e;
-    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
     DeviceState &st = g_states[dev];
     if (!st.sp) {
-        std::vector<SpEntry> tab;
-        build_sp_table(tab);
+        const HostTables &ht = host_tables();
+        const std::vector<SpEntry> &tab = ht.sp;
         SpEntry *sp = nullptr;
         e = hipMalloc(&sp, tab.size() * sizeof(SpEntry));
         if (e != hipSuccess) return e;
@@ -2895,23 +2926,19 @@ static hipError_t get_state(uint32_t chunk, int nsets, DeviceState *&out)
         if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dAnchor2), kBc7Anchor2, sizeof(kBc7Anchor2));
         if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dAnchor3a), kBc7Anchor3a, sizeof(kBc7Anchor3a));
         if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dAnchor3b), kBc7Anchor3b, sizeof(kBc7Anchor3b));
-        std::vector<uint32_t> prob, minpart;
-        std::vector<uint16_t> tsub;
-        const int nu = build_subset_problems(prob, minpart, tsub);
-        if (e == hipSuccess && nu > kUMax) e = hipErrorInvalidValue;
-        if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dUProb), prob.data(), prob.size() * sizeof(uint32_t));
+        if (e == hipSuccess && ht.nu > kUMax) e = hipErrorInvalidValue;
         if (e == hipSuccess)
-            e = hipMemcpyToSymbol(HIP_SYMBOL(dUMinPart), minpart.data(), minpart.size() * sizeof(uint32_t));
-        if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dTaskSub), tsub.data(), tsub.size() * sizeof(uint16_t));
-        std::vector<uint32_t> pairs;
-        const int nm = build_subset_masks(prob, pairs);
-        if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(dUMask), pairs.data(), pairs.size() * sizeof(uint32_t));
+            e = hipMemcpyToSymbol(HIP_SYMBOL(dUProb), ht.prob.data(), ht.prob.size() * sizeof(uint32_t));
+        if (e == hipSuccess)
+            e = hipMemcpyToSymbol(HIP_SYMBOL(dUMinPart), ht.minpart.data(), ht.minpart.size() * sizeof(uint32_t));
+        if (e == hipSuccess)
+            e = hipMemcpyToSymbol(HIP_SYMBOL(dTaskSub), ht.tsub.data(), ht.tsub.size() * sizeof(uint16_t));
+        if (e == hipSuccess)
+            e = hipMemcpyToSymbol(HIP_SYMBOL(dUMask), ht.pairs.data(), ht.pairs.size() * sizeof(uint32_t));
         if (e != hipSuccess) {
             (void)hipFree(sp);
             return e;
         }
-        g_nu = nu;
-        g_nm = nm;
         st.device = dev;
         st.sp = sp;
     }
@@ -3121,9 +3148,12 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
     // while holding the device lock: concurrent calls (other threads, other
     // caller streams) are serialised in lane order, never interleaved on a
     // workspace.  The caller's stream is joined by fork/join events.
-    std::lock_guard<std::mutex> lk(g_state_lock);
+    int dev = 0;
+    hipError_t e = current_device(dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(g_dev_lock[dev]);
     DeviceState *st = nullptr;
-    hipError_t e = get_state(chunk, nsets, st);
+    e = get_state(chunk, nsets, st);
     if (e != hipSuccess) return e;
     // BC7BlockEncoder ctor: m_performance clamped to [0, 1], m_quantizerRangeThreshold
     // = 255 * m_performance (amd_bc7_body.hpp:109-116)
@@ -3319,9 +3349,12 @@ hipError_t launch_bc7_decode(const uint8_t *blocks, uint32_t width, uint32_t hei
                              size_t row_pitch, hipStream_t s)
 {
     {   // the partition / anchor tables live in this library's constant memory
-        std::lock_guard<std::mutex> lk(bc7::g_state_lock);
+        int dev = 0;
+        hipError_t e = bc7::current_device(dev);
+        if (e != hipSuccess) return e;
+        std::lock_guard<std::mutex> lk(bc7::g_dev_lock[dev]);
         bc7::DeviceState *st = nullptr;
-        const hipError_t e = bc7::get_state(0, 0, st);
+        e = bc7::get_state(0, 0, st);
         if (e != hipSuccess) return e;
     }
     const uint32_t bx = (width + 3) / 4, by = (height + 3) / 4;
@@ -3346,14 +3379,15 @@ hipError_t launch_bc7_blocks(const float *blocks, uint32_t n, const gic_options 
 
 hipError_t bc7_nonterm(unsigned long long *n, int reset)
 {
-    std::lock_guard<std::mutex> lk(bc7::g_state_lock);
-    hipError_t e = hipMemcpyFromSymbol(n, HIP_SYMBOL(bc7::g_nonterm), sizeof(*n));
+    int dev = 0;
+    hipError_t e = bc7::current_device(dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(bc7::g_dev_lock[dev]);
+    e = hipMemcpyFromSymbol(n, HIP_SYMBOL(bc7::g_nonterm), sizeof(*n));
     if (e == hipSuccess && reset) {
         const unsigned long long z = 0;
         e = hipMemcpyToSymbol(HIP_SYMBOL(bc7::g_nonterm), &z, sizeof(z));
-        int dev = 0;
-        if (e == hipSuccess) e = hipGetDevice(&dev);
-        if (e == hipSuccess && dev >= 0 && dev < 64) bc7::g_states[dev].nonterm_seen = 0;
+        if (e == hipSuccess) bc7::g_states[dev].nonterm_seen = 0;
     }
     return e;
 }

@@ -123,6 +123,40 @@ int gic_hip_encode_rows_src(gic_format fmt, gic_source src_type, const void *d_s
                             uint32_t first_block_row, uint32_t num_block_rows, const gic_options *opt,
                             uint8_t *d_dst, double *d_block_err, void *stream);
 
+/* Multi-GPU encode from one host process (the split of the
+ * reference's block loop, amd_bc1_compressor.cpp:44-70 / amd_bc7_compressor.cpp:
+ * 48-77, across devices).  The block rows of every slice, numbered slice-major,
+ * are cut into `ndev` contiguous ranges (the first rows % ndev one row longer);
+ * device devices[i] uploads the source rows its range reads from the host image
+ * `h_src` (slices x height rows of row_pitch bytes) and encodes them on its own
+ * stream, every device from its own host thread; then ONE gather collects the
+ * packed blocks at their reference-order offsets in `d_dst_root`, device
+ * memory on devices[0] (ceil(w/4) * ceil(h/4) * slices * gic_block_bytes):
+ * grouped ncclSend / ncclRecv over RCCL communicators (ncclCommInitAll over
+ * the list, built once and kept until the list changes or gic_multi_release),
+ * or peer copies when the list names a device twice or flags has
+ * GIC_MULTI_PEER_COPY.  Returns after the gather completed; the calling
+ * thread's current device is preserved.  Image_CompressAMD* use it when the
+ * environment variable GIC_DEVICES lists more than one device (e.g. "0,1,2,3")
+ * and no progress callback is given. */
+#define GIC_MULTI_PEER_COPY 1u
+typedef struct gic_multi_report {
+    int ranks;               /* devices in the list */
+    int rccl;                /* 1: the gather ran over RCCL, 0: peer copies */
+    double encode_ms_max;    /* the slowest device's upload + encode (HIP events on its stream) */
+    double gather_ms;        /* the gather on the root's stream */
+    uint64_t gathered_bytes; /* packed bytes received from the other devices */
+} gic_multi_report;
+int gic_encode_multi(gic_format fmt, gic_source src_type, const void *h_src, uint32_t width, uint32_t height,
+                     uint32_t slices, uint32_t channels, size_t row_pitch, const gic_options *opt, int ndev,
+                     const int *devices, uint8_t *d_dst_root, uint32_t flags);
+/* the calling thread's last gic_encode_multi */
+int gic_multi_last_report(gic_multi_report *out);
+/* frees the device-list state (communicators, streams, buffers) */
+int gic_multi_release(void);
+/* the split: device i's first slice-major block row and row count (host only) */
+int gic_multi_split(uint64_t rows_total, int ndev, int i, uint64_t *first, uint64_t *rows);
+
 /* Block-level batch: n blocks of 16 texels, float in [0,1].
  *   BC1/BC2/BC3/BC7: d_blocks holds n x 64 floats (RGBA per texel, texel-major).
  *   BC4:     d_blocks holds n x 16 floats.

@@ -250,3 +250,13 @@ def test_bench_gpus_flag_launches_ranks(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8"])
     with pytest.raises(SystemExit):
         bench.relaunch_if_needed(bench.parse())
+
+
+def test_c_abi_multi_split_matches_shard_rows():
+    """gic_encode_multi's split of the slice-major block rows (the C ABI's
+    multi-GPU path, gic_multi.cpp) is shard.shard_rows: the same contiguous
+    ranges bench.py and the torch.distributed path use.  Host-only, no GPU."""
+    import gfx_imagecompress_amd as gic
+    for rows in list(range(0, 70)) + [2048, 2048 * 64, 1024 * 64 + 5]:
+        for n in range(1, 9):
+            assert [gic.multi_split(rows, n, i) for i in range(n)] == [shard.shard_rows(rows, n, i) for i in range(n)]
