@@ -932,7 +932,7 @@ static double shake_window(double data[][4], int n, int *index_, int epo_code[2]
                 double epa[2][4];
                 for (int k = 0; k < n; ++k) cidx[k] = index[k] * q + p;
                 ls_endpoints(data, cidx, n, last, dim, epa);
-                double err1 = DBL_MAX, ed[2][2][4]; ST(7, 1);
+                double err1 = DBL_MAX, ed[2][2][4]; ST(7, 1); ST(60, n); ST(61, Mi + 1);
 #ifdef ORC_STATS
                 {
                     unsigned long long sig = 0, sig1 = 0;

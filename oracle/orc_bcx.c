@@ -11,6 +11,9 @@
  * (amd_bcx_body.cpp:60-63).
  */
 #include "bcn_oracle.h"
+#ifdef ORC_STATS
+__thread long orc_bcx_stat[4];   /* study counters (tools/bc1_iter_study.c) */
+#endif
 
 #include <float.h>
 #include <math.h>
@@ -462,6 +465,9 @@ static void fit_endpoints(float result[3][2], float blkin[16][4], const float rp
         float dir[3] = {dir0[0], dir0[1], dir0[2]}, dir_g[3] = {0, 0, 0}, pos_g[2] = {0, 0};
         float prj0[16], prj[16], perr[16], prem[16], ridx[16];
         for (;;) {
+#ifdef ORC_STATS
+            orc_bcx_stat[n == 3 ? 0 : 1]++;   /* axis-loop iterations of the 3- / 4-colour search */
+#endif
             float bnd[2] = {1000.f, -1000.f};
             for (int i = 0; i < 16; ++i)
                 prj0[i] = prj[i] = perr[i] = prem[i] = 0.f;
