@@ -3020,14 +3020,17 @@ static hipError_t get_state(uint32_t chunk, int nsets, DeviceState *&out)
 // f64 fallback kernels (k_quant, k_shake, k_dual_quant, k_dual) would only
 // read the flags and exit; they are not launched (their 1-wave/SIMD grids
 // otherwise wait for whole SIMDs behind the other lane's shakers).
-static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, hipStream_t s, bool integral)
+static hipError_t run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, hipStream_t s, bool integral)
 {
     const uint32_t wg = 256;
     const uint32_t sm = p.stage_mask;
     const bool single = (sm & 0xCFu) != 0, dual = (sm & 0x30u) != 0;
     // deferred shake problems of this pass (fast wave kernels -> slow ones);
-    // the slow kernels' grid: 4 waves per SIMD (their VGPRs allow 4), striding over the lists
-    (void)hipMemsetAsync(ws.defer_cnt, 0, 4 * sizeof(uint32_t), s);
+    // the slow kernels' grid: 4 waves per SIMD (their VGPRs allow 4), striding
+    // over the lists.  The counters must be zero before the fast kernels
+    // append: a failed reset stops the pass.
+    const hipError_t me = hipMemsetAsync(ws.defer_cnt, 0, 4 * sizeof(uint32_t), s);
+    if (me != hipSuccess) return me;
     const dim3 slow_grid(1024);
     if (single) {
         const uint64_t nq = (uint64_t)p.n * kQuantTasks;
@@ -3085,6 +3088,7 @@ static void run_modes(const Params &p, const Workspace &ws, const SpEntry *sp, h
         hipLaunchKernelGGL(k_dual_wave, dim3((uint32_t)((ndw + wg - 1) / wg)), dim3(wg), 0, s, p, ws, sp);
         hipLaunchKernelGGL(k_dual_wave_slow, slow_grid, dim3(wg), 0, s, p, ws, sp);
     }
+    return hipGetLastError();
 }
 
 #ifndef GIC_BC7_CHUNK
@@ -3202,18 +3206,22 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
             if (valid_modes & (1u << order[k])) stages[nstages++] = k;
     stages[nstages++] = -1;   // the search itself
     // the search over one chunk (the modes in one launch sequence, or staged)
-    auto search = [&](Params p, const Workspace &ws, hipStream_t s, bool integral) {
+    auto search = [&](Params p, const Workspace &ws, hipStream_t s, bool integral) -> hipError_t {
         int resume = 0;
         for (int k = 0; k < (staged ? 8 : 1); ++k) {
             p.stage_mask = staged ? (1u << order[k]) : 0xFFu;
             const bool last = !staged || k == 7;
             const bool skip = staged && !(valid_modes & p.stage_mask);
             if (skip && !last) continue;
-            if (!skip) run_modes(p, ws, st->sp, s, integral);
+            if (!skip) {
+                const hipError_t re = run_modes(p, ws, st->sp, s, integral);
+                if (re != hipSuccess) return re;
+            }
             hipLaunchKernelGGL(k_select, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, p, ws, (uint4 *)dst, err,
                                staged ? k : 0, staged ? k + 1 : 8, resume);
             resume = 1;
         }
+        return hipGetLastError();
     };
     const uint32_t *cur = nullptr;
     uint32_t cur_n = total;
@@ -3241,14 +3249,16 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
                 pp.bound_sse = 64.0 * (double)o.bc7_mse_bound;
                 pp.probe = 1;
                 pp.stage_mask = 1u << order[pk];
-                run_modes(pp, ws, st->sp, s, g != nullptr);
+                e = run_modes(pp, ws, st->sp, s, g != nullptr);
+                if (e != hipSuccess) return e;
                 hipLaunchKernelGGL(k_select, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, pp, ws, (uint4 *)dst, err,
                                    pk, pk + 1, 0);
                 hipLaunchKernelGGL(k_bound, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, pp, ws, (uint4 *)dst, err);
                 hipLaunchKernelGGL(k_compact, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, pp, ws, out,
                                    st->count + si);
             } else {
-                search(p, ws, s, g != nullptr);
+                e = search(p, ws, s, g != nullptr);
+                if (e != hipSuccess) return e;
             }
             e = hipGetLastError();
             if (e != hipSuccess) return e;
@@ -3288,8 +3298,7 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
                 hipLaunchKernelGGL(k_prep_image, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, *g, p, ws);
             else
                 hipLaunchKernelGGL(k_prep_f32, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, blocks, p, ws);
-            search(p, ws, s, false);
-            e = hipGetLastError();
+            e = search(p, ws, s, false);
             if (e != hipSuccess) return e;
         }
         e = hipStreamSynchronize(st->lane[0]);

@@ -93,14 +93,17 @@ struct Res {            // color_cell_compressor_results :297-305
 // 256 lanes wide, so a wave's reads are conflict-free).  Held in registers
 // they were 48 VGPRs live through the whole search (2 waves per SIMD); the
 // read address is opaque at every use so the loads stay inside the ramp loops.
+// (STRIDE = the workgroup's lanes: 256 for the lane-per-block kernels, 64 for
+// the one-wave block kernel, whose 48 rows then take 12 KB instead of 48 KB)
 constexpr uint32_t kYccStride = 256;
-struct Ycc {
+template <uint32_t STRIDE>
+struct YccT {
     uint32_t a;   // LDS byte address of this lane's row-0 word
     __device__ __forceinline__ int at(int row) const
     {
         uint32_t b = a;
         asm volatile("" : "+v"(b));
-        return *(const __attribute__((address_space(3))) int *)(size_t)(b + 4u * (uint32_t)row * kYccStride);
+        return *(const __attribute__((address_space(3))) int *)(size_t)(b + 4u * (uint32_t)row * STRIDE);
     }
     __device__ __forceinline__ int l(int i) const { return at(i); }
     __device__ __forceinline__ int cr(int i) const { return at(16 + i); }
@@ -108,11 +111,12 @@ struct Ycc {
     __device__ __forceinline__ void put(int i, int l_, int cr_, int cb_) const
     {
         typedef __attribute__((address_space(3))) int lds_i32;
-        *(lds_i32 *)(size_t)(a + 4u * (uint32_t)i * kYccStride) = l_;
-        *(lds_i32 *)(size_t)(a + 4u * (uint32_t)(16 + i) * kYccStride) = cr_;
-        *(lds_i32 *)(size_t)(a + 4u * (uint32_t)(32 + i) * kYccStride) = cb_;
+        *(lds_i32 *)(size_t)(a + 4u * (uint32_t)i * STRIDE) = l_;
+        *(lds_i32 *)(size_t)(a + 4u * (uint32_t)(16 + i) * STRIDE) = cr_;
+        *(lds_i32 *)(size_t)(a + 4u * (uint32_t)(32 + i) * STRIDE) = cb_;
     }
 };
+using Ycc = YccT<kYccStride>;
 
 // scale_color :307-323 (n = component bits + p-bit)
 __device__ __forceinline__ uint32_t expand(uint32_t q, uint32_t n)
@@ -179,10 +183,10 @@ __device__ __forceinline__ uint64_t nibble_mask(uint32_t m)
 // a problem's result is updated only if want[s] (find_optimal_solution's
 // changed-endpoints test).  Texels outside a K = 1 problem's mask are computed
 // and discarded (branch-free); the integer totals do not depend on order.
-template <bool P, int K>
+template <bool P, int K, class Y = Ycc>
 __device__ __forceinline__ void evaluate(const uint32_t lo[K], const uint32_t hi[K], const uint32_t pb0[K],
                                          const uint32_t pb1[K], const bool want[K], const Prob pr[K], uint32_t m0,
-                                         const uint32_t px[16], const Ycc &tx, const EncCfg &cf, Res r[K])
+                                         const uint32_t px[16], const Y &tx, const EncCfg &cf, Res r[K])
 {
     uint32_t a[K], b[K];
 #pragma unroll
@@ -384,9 +388,9 @@ __device__ __forceinline__ void quantize(float xl[4], float xh[4], const Prob &p
 
 // find_optimal_solution for the K problems: quantise each active one's
 // endpoints, evaluate those that differ from its best (:710, :724)
-template <bool P, int K>
+template <bool P, int K, class Y = Ycc>
 __device__ __forceinline__ void fit(float xl[K][4], float xh[K][4], const bool active[K], const Prob pr[K],
-                                    uint32_t m0, const uint32_t px[16], const Ycc &tx, const EncCfg &cf, Res r[K])
+                                    uint32_t m0, const uint32_t px[16], const Y &tx, const EncCfg &cf, Res r[K])
 {
     uint32_t lo[K], hi[K], p0[K], p1[K];
     bool want[K], any = false;
@@ -454,8 +458,8 @@ __device__ __forceinline__ void lsq(const Prob pr[K], uint32_t m0, uint64_t sel,
 }
 
 // pack_mode1_to_one_color :357-403
-template <bool P>
-__device__ __forceinline__ void one_colour(uint32_t cr, uint32_t cg, uint32_t cb, const Prob &pr, const uint32_t px[16], const Ycc &tx,
+template <bool P, class Y = Ycc>
+__device__ __forceinline__ void one_colour(uint32_t cr, uint32_t cg, uint32_t cb, const Prob &pr, const uint32_t px[16], const Y &tx,
                            const EncCfg &cf, const EncLds &L, Res &r)
 {
     uint32_t best = kNone, bp = 0;
@@ -614,8 +618,8 @@ __device__ __forceinline__ void pca_endpoints(const Prob &pr, const uint32_t px[
 }
 
 // color_cell_compression :731-1024 for K problems in lockstep
-template <bool P, int K>
-__device__ __forceinline__ void cells(const Prob pr[K], uint32_t m0, const uint32_t px[16], const Ycc &tx,
+template <bool P, int K, class Y = Ycc>
+__device__ __forceinline__ void cells(const Prob pr[K], uint32_t m0, const uint32_t px[16], const Y &tx,
                                       const EncCfg &cf, const EncLds &L, Res r[K])
 {
     bool fin[K];   // the subset was packed as one colour (:738-754): no trials
@@ -767,8 +771,8 @@ __device__ __forceinline__ void est_setup(EstSubset &e)
 // are non-negative and the caller keeps a total only if it is strictly less),
 // so the sum stops -- the reference's own early exit (:1156-1157), taken per
 // wave after every two texels.
-template <bool P>
-__device__ __forceinline__ uint32_t estimate2(uint32_t m0, const uint32_t px[16], const Ycc &tx, const EncCfg &cf,
+template <bool P, class Y = Ycc>
+__device__ __forceinline__ uint32_t estimate2(uint32_t m0, const uint32_t px[16], const Y &tx, const EncCfg &cf,
                                               uint32_t best)
 {
     EstSubset s0, s1;
@@ -831,8 +835,8 @@ __device__ __forceinline__ uint32_t shape_mask(uint32_t shape, uint32_t subset)
 }
 
 // estimate_partition :1207-1281
-template <bool P>
-__device__ __forceinline__ uint32_t pick_partition(const uint32_t px[16], const Ycc &tx, const EncCfg &cf)
+template <bool P, class Y = Ycc>
+__device__ __forceinline__ uint32_t pick_partition(const uint32_t px[16], const Y &tx, const EncCfg &cf)
 {
     const uint32_t total = cf.max_parts < 64 ? cf.max_parts : 64;
     if (total <= 1) return 0;
@@ -858,8 +862,8 @@ __device__ __forceinline__ uint32_t pick_partition(const uint32_t px[16], const 
 // wave, every lane holding it): lane it sums shape kEncPartOrder[it] in full, then
 // the reference's sequential choice (filter bank, stop rules, '<' keeps the
 // first) runs over those totals -- full sums are equivalent (see estimate2).
-template <bool P>
-__device__ __forceinline__ uint32_t pick_partition_wave(const uint32_t px[16], const Ycc &tx, const EncCfg &cf)
+template <bool P, class Y = Ycc>
+__device__ __forceinline__ uint32_t pick_partition_wave(const uint32_t px[16], const Y &tx, const EncCfg &cf)
 {
     const uint32_t total = cf.max_parts < 64 ? cf.max_parts : 64;
     if (total <= 1) return 0;
@@ -952,8 +956,8 @@ __device__ __forceinline__ uint4 pack_block(bool mode1, uint32_t part, uint64_t 
 // bc7enc16_compress_block :1517-1547 with handle_alpha_block / handle_opaque_block
 // :1390-1515 (m_endpoints_share_pbit, uninitialised for alpha blocks in the
 // reference, is false: mode 6 has a p-bit per endpoint)
-template <bool P, bool WAVE = false>
-__device__ __forceinline__ uint4 encode_block(const uint32_t px[16], const EncCfg &cf, const EncLds &L, Ycc tx)
+template <bool P, bool WAVE = false, class Y = Ycc>
+__device__ __forceinline__ uint4 encode_block(const uint32_t px[16], const EncCfg &cf, const EncLds &L, Y tx)
 {
     if (P) {
 #pragma unroll
@@ -1070,9 +1074,9 @@ __global__ void __launch_bounds__(64) bc7enc_blocks_wave_kernel(const uint4 *__r
                                                                 uint4 *__restrict__ dst)
 {
     __shared__ EncLds L;
-    __shared__ int ytab[P ? 48 * kYccStride : 1];
+    __shared__ int ytab[P ? 48 * 64 : 1];
     load_tables(L);
-    const Ycc tx{(uint32_t)(uintptr_t)(const __attribute__((address_space(3))) int *)(ytab + (P ? threadIdx.x : 0))};
+    const YccT<64> tx{(uint32_t)(uintptr_t)(const __attribute__((address_space(3))) int *)(ytab + (P ? threadIdx.x : 0))};
     const uint32_t id = blockIdx.x;
     if (id >= n) return;
     uint32_t px[16];

@@ -1,6 +1,6 @@
 # A/B timing of BC7 library variants (exact search on 256 block rows of the 8K
 # G1 texture, and the bounded exit over the whole 8K), in-tree library first,
-# each variant from gpurun_dbg/<variant>/lib.so, twice in alternation; then the
+# each variant from gpurun_var/<variant>/lib.so, twice in alternation; then the
 # BC7 GPU tests (pytest -k expression, default "bc7") on the in-tree library.
 #   bash tools/ab_bc7x.sh <tag> "<pytest -k>" <variant>...   -> gpurun_out/ab_<tag>/
 set -o pipefail
@@ -11,7 +11,7 @@ mkdir -p $O
 cd $R
 for rep in 1 2; do
   for v in default "$@"; do
-    if [ "$v" = default ]; then L=""; else L=$R/gpurun_dbg/$v/lib.so; fi
+    if [ "$v" = default ]; then L=""; else L=$R/gpurun_var/$v/lib.so; fi
     echo "== $v" >> $O/bc7.txt
     GIC_LIBRARY=$L timeout -k 10 300 python3 tools/time_bc7_bounded.py --rows 256 --bound 0 >> $O/bc7.txt 2>&1 || exit 1
     GIC_LIBRARY=$L timeout -k 10 300 python3 tools/time_bc7_bounded.py --rows 2048 --bound 0.5 >> $O/bc7.txt 2>&1 || exit 1
