@@ -566,6 +566,21 @@ __device__ __forceinline__ float proj_ramp_error(float error, const float prj[16
     return error;
 }
 
+// proj_ramp_error over entries [8, 8 + live): `live` (wave-uniform) counts the
+// entries past 8 that some lane of the wave still has (unique colours n > i);
+// the rest add +0 on every lane and are not evaluated.  (G1: a wave's largest
+// n is 13-16, so 1.4 of 16 entries go; tools/bc1_cut_study.c.)
+__device__ __forceinline__ float proj_ramp_error_tail(float error, const float prj[16], const float perr[16],
+                                                      const float prem[16], const RampStep &r, int live)
+{
+#pragma unroll
+    for (int i = 8; i < 16; ++i) {
+        if (i - 8 >= live) break;
+        error = proj_ramp_error<0, 1>(error, prj + i, perr + i, prem + i, r);
+    }
+    return error;
+}
+
 // FindAxis, amd_bcx_body.cpp:442-570.  The centred colours sh = blk - centre
 // are recomputed where needed (bit-identical each time) instead of stored.
 template <class Col>
@@ -748,6 +763,10 @@ __device__ __forceinline__ void fit_endpoints(float result[3][2], const Col &u, 
                     pos1 = __shfl(hp, o);
                 }
             } else {
+            // entries past 8 that any lane of the wave still has (uniform)
+            int live = 0;
+#pragma unroll
+            for (int i = 8; i < 16; ++i) live += __any(u.n > i) ? 1 : 0;
             float lp = ls;
             for (int l = 0; l < 8; ++l, lp += stp) {
                 float hp = he;
@@ -757,7 +776,7 @@ __device__ __forceinline__ void fit_endpoints(float result[3][2], const Col &u, 
                     // cannot make this candidate win (RampSrchW's own early out)
                     const RampStep rs = ramp_step<N>(lp, hp);
                     float e = proj_ramp_error<0, 8>(0.f, prj, perr, prem, rs);
-                    if (!__all(e >= err)) e = proj_ramp_error<8, 16>(e, prj, perr, prem, rs);
+                    if (!__all(e >= err)) e = proj_ramp_error_tail(e, prj, perr, prem, rs, live);
                     if (e < err) {
                         err = e;
                         pos0 = lp;
@@ -1829,11 +1848,15 @@ __global__ void __launch_bounds__(256, 2) bc23_image_kernel(Geometry g, int fmt,
 // texels as packed bytes (row loads of 4 / 8 / 16 bytes for 1 / 2 / 4
 // channels), each selected byte to v / 255.0f through a 256-entry LDS table.
 // (A float RGBA gather indexed by a runtime channel went to scratch: 608 bytes
-// per lane.)  Budgeted for 6 waves/SIMD (BC4, 80 VGPRs, one spilled) and 5
-// (BC5, 96, four spilled): 8K BC4 0.261 -> 0.255 ms, BC5 0.924 -> 0.859 ms against
-// the unconstrained 81 / 97-VGPR build, same blocks (profiles/r04f_bc45_ab.txt).
+// per lane.)  Budgeted for 6 waves/SIMD: without SLP vectorisation (Makefile)
+// BC4 takes 67 VGPRs (7 waves) and BC5 fits 6 waves (83 -> 80 VGPRs, no spill):
+// 8K BC5 0.86 -> 0.83 ms, same blocks (profiles/r05_noslp_ab.txt).  (Round 4:
+// 6 / 5 waves with spills, BC4 0.261 -> 0.255, BC5 0.924 -> 0.859 ms.)  BC5's two
+// halves on neighbouring lanes instead -- twice the waves, one channel each --
+// ran 1.08 ms: a wave lasts as long as its slowest lane, and the channels' search
+// lengths vary, so 64 (R + G) chains finish sooner than 2 x 32 max(R, G) ones.
 template <int FMT>
-__global__ void __launch_bounds__(256, FMT == 4 ? 6 : 5) bc45_image_kernel(Geometry g, int channel, uint64_t *__restrict__ dst)
+__global__ void __launch_bounds__(256, 6) bc45_image_kernel(Geometry g, int channel, uint64_t *__restrict__ dst)
 {
     __shared__ float lut[256];   // byte -> v / 255.0f
     __shared__ float wk_uv[16 * 256];     // CompBlock1's uv of each lane

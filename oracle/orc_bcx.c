@@ -13,6 +13,9 @@
 #include "bcn_oracle.h"
 #ifdef ORC_STATS
 __thread long orc_bcx_stat[4];   /* study counters (tools/bc1_iter_study.c) */
+/* study hook: every RampSrchW call's running sums without the early break
+ * (tools/bc1_cut_study.c) */
+void (*orc_bcx_ramp_hook)(const float run[16], const float perr[16], float maxerr, int ncol, int n);
 #endif
 
 #include <float.h>
@@ -186,6 +189,26 @@ static float proj_ramp_error(const float *prj, const float *perr, const float *r
     const float step = (hi - lo) / (float)(n - 1);
     const float step_h = step * (float)0.5;
     const float rstep = (float)1.0f / step;
+#ifdef ORC_STATS
+    if (orc_bcx_ramp_hook) {
+        float run[16] = {0}, acc = 0;
+        for (int i = 0; i < ncol; ++i) {
+            float v, del;
+            if ((del = prj[i] - lo) <= 0)
+                v = lo;
+            else if (prj[i] - hi >= 0)
+                v = hi;
+            else
+                v = floorf((del + step_h) * rstep) * step + lo;
+            float d = prj[i] - v;
+            d *= d;
+            acc += rpt[i] * d + perr[i];
+            run[i] = acc;
+        }
+        for (int i = ncol; i < 16; ++i) run[i] = acc;
+        orc_bcx_ramp_hook(run, perr, maxerr, ncol, n);
+    }
+#endif
     for (int i = 0; i < ncol; ++i) {
         float v, del;
         if ((del = prj[i] - lo) <= 0)

@@ -75,8 +75,8 @@ def test_bc7_fast_shakers_run_eight_waves(res):
 
 def test_bc4_bc5_image_kernels_use_no_scratch_arrays(res):
     """CompBlock1's running arrays live in LDS columns, not scratch; the kernels
-    run 6 (BC4) and 5 (BC5) waves per SIMD with at most a few spilled VGPRs."""
-    for part, waves in (("bc45_image_kernelILi4E", 6), ("bc45_image_kernelILi5E", 5)):
+    run at least 6 waves per SIMD with at most a few spilled VGPRs."""
+    for part, waves in (("bc45_image_kernelILi4E", 6), ("bc45_image_kernelILi5E", 6)):
         r = _kernel(res, part)
         assert r["waves"] >= waves and r["private"] <= 32 and r["vgpr_spill"] <= 4, (part, r)
 

@@ -4,7 +4,7 @@
 set -e
 NAME=$1; WAVE=$2; HIP=$3; shift 3
 D=/root/repo/gfx_imagecompress_amd
-F="-I../include -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero -fno-fast-math"
+F="-I../include -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero -fno-fast-math -fno-slp-vectorize"
 cd $D
 cp $WAVE csrc/_v_wave.inc
 cp ${QUANT_INC:-csrc/bc7_quant.inc} csrc/_v_quant.inc
