@@ -5,7 +5,8 @@
 Writes <tag>_bench.json, <tag>_bench_under_rocprof.json, <tag>_kernel_stats.csv,
 <tag>_pmc_valu.csv, <tag>_pmc_valu_bc7.csv, <tag>_bc7_kernel_stats_single_stream.csv,
 <tag>_pmc_{fetch,write}_size.csv and regenerates valu_bc1.json, valu_bc7enc16*.json,
-valu_bc7_{shake8,shake4,dual_wave,quant_sub}.json, valu_bc7*_pass.json, traffic_bc1.json.
+valu_bc7_{shake8,shake4,dual_wave,quant_sub}.json, valu_bc7*_pass.json, valu_bc6h_shake*.json,
+traffic_bc1.json.
 """
 import csv
 import json
@@ -43,6 +44,11 @@ def main():
                         f"{leg}: 8K G1 one pass, shake ranks {k}, bound {bound}", "--command",
                         f"tools/time_bc7_bounded.py --rows 2048 --shake-ranks {k} --bound {bound} --no-warm"],
                        check=True)
+    p6 = os.path.join(ROOT, "gpurun_out", f"p6_{tag}")
+    for k, out in (("unsigned", "valu_bc6h_shake.json"), ("signed", "valu_bc6h_shake_signed.json")):
+        if os.path.isdir(os.path.join(p6, k)):
+            subprocess.run([py, os.path.join(ROOT, "tools", "valu_bc6h_json.py"), os.path.join(p6, k),
+                            os.path.join(P, out), "--size", "1024"], check=True)
     f, nf = per_launch(os.path.join(pr, "pmc_fetch", "run_counter_collection.csv"), "bc1_image_kernel", "FETCH_SIZE")
     w, _ = per_launch(os.path.join(pr, "pmc_write", "run_counter_collection.csv"), "bc1_image_kernel", "WRITE_SIZE")
     tj = os.path.join(P, "traffic_bc1.json")

@@ -3,7 +3,8 @@
 #                                             command under rocprofv3 --kernel-trace --stats
 #   bash tools/profile_r05.sh <tag> pmc    -> SQ issue counters of the bench legs and of the exact BC7 search
 #       (64 block rows, one stream, with its kernel trace), BC1 FETCH_SIZE / WRITE_SIZE passes, the
-#       one-pass VALU totals of the four BC7 8K legs, and the block-call latencies
+#       one-pass VALU totals of the four BC7 8K legs, the BC6H per-kernel time and SQ counters
+#       (tools/prof_bc6h_r04.sh -> gpurun_out/p6_<tag>/), and the block-call latencies
 set -o pipefail
 TAG=${1:-r05}
 WHAT=${2:-bench}
@@ -28,6 +29,7 @@ for leg in "bc7 0 0" "bc7_pruned 2 0" "bc7_bounded 0 0.5" "bc7_bounded_pruned 2 
   set -- $leg
   timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $O/pass_$1 -o run -- python3 $R/tools/time_bc7_bounded.py --rows 2048 --shake-ranks $2 --bound $3 --no-warm > $O/pass_$1.log 2>&1 || { tail -20 $O/pass_$1.log; exit 1; }
 done
+bash $R/tools/prof_bc6h_r04.sh $TAG > $O/bc6h.txt 2>&1 || { tail -20 $O/bc6h.txt; exit 1; }
 cd $R
 if [ -x gpurun_var/block_latency ]; then timeout -k 10 120 ./gpurun_var/block_latency 2000 > $O/block_latency.txt 2>&1 || exit 1; cat $O/block_latency.txt; fi
 echo done
