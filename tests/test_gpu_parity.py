@@ -91,6 +91,35 @@ def test_bc1_bc5_channel_layouts(gpu, channels):
         assert np.array_equal(out, ref), (fmt, _mismatch_report(out, ref))
 
 
+def _k_colour_blocks(bx, by, kmax, seed):
+    """An image whose block (x, y) has exactly k = k(x, y) distinct colours,
+    k in 1..kmax: each texel takes one of the block's k random palette entries,
+    every entry used at least once."""
+    rng = np.random.default_rng(seed)
+    img = np.zeros((by * 4, bx * 4, 4), np.uint8)
+    img[..., 3] = 255
+    for y in range(by):
+        for x in range(bx):
+            k = int(rng.integers(1, kmax + 1))
+            pal = rng.integers(0, 256, size=(k, 3), dtype=np.uint8)
+            sel = np.concatenate([np.arange(k), rng.integers(0, k, size=16 - k)])
+            rng.shuffle(sel)
+            img[y * 4:(y + 1) * 4, x * 4:(x + 1) * 4, :3] = pal[sel].reshape(4, 4, 3)
+    return img
+
+
+@pytest.mark.parametrize("kmax", [3, 8, 9, 12, 16])
+def test_bc1_wave_unique_colour_counts(gpu, kmax):
+    """The 8x8 endpoint search evaluates entries only up to the largest unique-
+    colour count of the wave's blocks (64 consecutive blocks of a block row):
+    waves whose blocks all have <= 8 colours skip the whole second half, waves
+    mixing 1..kmax stop at the largest.  Bit-exact against the oracle either way."""
+    img = _k_colour_blocks(128, 6, kmax, seed=kmax)
+    out = gpu_encode(gic.FMT_BC1, img)
+    ref = oracle_lib.encode_image(1, img)
+    assert np.array_equal(out, ref), _mismatch_report(out, ref)
+
+
 def test_bc1_solid_and_transparent_blocks(gpu):
     img = np.zeros((16, 16, 4), np.uint8)
     img[:8, :8] = (10, 200, 30, 255)        # solid colour
