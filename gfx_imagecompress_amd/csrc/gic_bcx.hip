@@ -1526,15 +1526,21 @@ __device__ __forceinline__ void bc4_sort(const float v[16], float s[16])
 #pragma unroll
     for (int i = 0; i < 16; ++i) nan = nan || v[i] != v[i];
     if (!nan) {
+        // ranks first, then each slot gathers its texel through a select chain
+        // (a scatter s[r] = v[i] became a dynamically indexed scratch store)
+        int r[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            int r = 0;
+            r[i] = 0;
 #pragma unroll
-            for (int j = 0; j < 16; ++j) r += (v[j] < v[i] || (v[j] == v[i] && j < i)) ? 1 : 0;
-            // scatter through a select chain keeps s[] in registers
+            for (int j = 0; j < 16; ++j) r[i] += (v[j] < v[i] || (v[j] == v[i] && j < i)) ? 1 : 0;
+        }
 #pragma unroll
-            for (int k = 0; k < 16; ++k)
-                if (r == k) s[k] = v[i];
+        for (int k = 0; k < 16; ++k) {
+            float x = v[0];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) x = (r[i] == k) ? v[i] : x;
+            s[k] = x;
         }
     } else {
         // A NaN texel (float sources only): QSortFCmp (:1609-1618) calls a NaN
@@ -1621,35 +1627,67 @@ __device__ uint64_t encode_bc4(const float v[16], W wk = W())
 // recovered by a (error, order) minimum.  Every ramp error is the same function
 // of the same floats as in scalar_endpoints, so the blocks are bit-identical.
 
-template <int N, bool FIXED>
-__device__ void scalar_endpoints_wave(float ramp[2], const float vals_sorted[16], float *uv, float *ur)
+// The block's unique values (uv) and repeat counts (ur) as register arrays:
+// every lane holds the same block, so they are built with static indices --
+// the round-4 version kept them in LDS and read two LDS words per entry inside
+// rolled loops, which one wave cannot hide (BC4 block kernel 39 us).  Entries
+// past nu hold uv = 0, ur = 0 and add +0 to every ramp error.
+template <int N>
+__device__ __forceinline__ float scalar_ramp_error_reg(const float uv[16], const float ur[16], float lo, float hi)
 {
-    // compaction: uniform, every lane writes the same values (uv / ur in LDS)
+    float error = 0;
+    const float step = (hi - lo) / (float)(N - 1);
+    const float step_h = step * 0.5f;
+    const float rstep = 1.0f / step;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        float q, del;
+        if ((del = uv[i] - lo) <= 0)
+            q = lo;
+        else if (uv[i] - hi >= 0)
+            q = hi;
+        else
+            q = (floorf((del + step_h) * rstep) * step) + lo;
+        const float d = uv[i] - q;
+        error += d * d * ur[i];
+    }
+    return error;
+}
+
+template <int N, bool FIXED>
+__device__ __forceinline__ void scalar_endpoints_wave(float ramp[2], const float vals_sorted[16])
+{
+    // compaction, scalar_endpoints' loop restated over runs of equal sorted
+    // values: a run starts where a value differs from its predecessor (from
+    // -2.f before the first, as the loop's `prev`; a NaN always differs), FIXED
+    // keeps a run only strictly inside (1.5/255, 253.5/255); entry k is the k-th
+    // kept run, its value and length.  (A leading run equal to -2.f is dropped:
+    // the loop's out-of-range ur[-1] increment, undefined in the reference.)
+    float uv[16], ur[16];
+    bool st[16], kp[16];
+    int rk[16];
     int nu = 0;
-    float prev = -2.f;
+    bool started = false;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const float x = vals_sorted[i];
-        if (FIXED) {
-            if (prev != x) {
-                prev = x;
-                if (!((double)prev <= 1.5 / 255.) && !((double)prev >= 253.5 / 255.)) {
-                    uv[nu] = x;
-                    ur[nu] = 1.f;
-                    nu++;
-                }
-            } else if (nu > 0 && uv[nu - 1] == prev) {
-                ur[nu - 1] += 1.f;
-            }
-        } else {
-            if (prev != x) {
-                uv[nu] = prev = x;
-                ur[nu] = 1.f;
-                nu++;
-            } else {
-                ur[nu - 1] += 1.f;
-            }
+        st[i] = x != (i == 0 ? -2.f : vals_sorted[i - 1]);
+        started = started || st[i];
+        const bool in = !FIXED || (!((double)x <= 1.5 / 255.) && !((double)x >= 253.5 / 255.));
+        kp[i] = started && in;
+        nu += (st[i] && in) ? 1 : 0;
+        rk[i] = nu - 1;   // the entry of this texel's run (if kept)
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        float v = 0.f, c = 0.f;
+#pragma unroll
+        for (int i = k; i < 16; ++i) {
+            v = (st[i] && kp[i] && rk[i] == k) ? vals_sorted[i] : v;
+            c += (kp[i] && rk[i] == k) ? 1.f : 0.f;
         }
+        uv[k] = v;
+        ur[k] = c;
     }
     if (nu <= 2) {
         if (FIXED && nu == 0) {
@@ -1661,7 +1699,9 @@ __device__ void scalar_endpoints_wave(float ramp[2], const float vals_sorted[16]
         }
     } else {
         const int ln = (int)(threadIdx.x & 63u);
-        float lo = uv[0], hi = uv[nu - 1];
+        float lo = uv[0], hi = uv[0];
+#pragma unroll
+        for (int k = 1; k < 16; ++k) hi = (k == nu - 1) ? uv[k] : hi;
         float lr = lo, hr = hi;
         const float cntr = (lr + hr) / 2;
         float gerr = 128000.f;
@@ -1681,7 +1721,7 @@ __device__ void scalar_endpoints_wave(float ramp[2], const float vals_sorted[16]
                 float sl = llb, sr = rrb;
                 for (int k = 0; k < i; ++k) sl += 0.018f;
                 for (int k = 0; k < j; ++k) sr -= 0.018f;
-                const float e = scalar_ramp_error<N>(uv, ur, sl, sr, nu);
+                const float e = scalar_ramp_error_reg<N>(uv, ur, sl, sr);
                 if (e < 128000.f && e < be) {   // first strictly smaller, per lane in loop order
                     be = e;
                     bo = t;
@@ -1714,7 +1754,7 @@ __device__ void scalar_endpoints_wave(float ramp[2], const float vals_sorted[16]
             float e = __builtin_huge_valf();
             int o = 0x7fffffff;
             if (ln < 9) {
-                const float t = scalar_ramp_error<N>(uv, ur, ca, cb, nu);
+                const float t = scalar_ramp_error_reg<N>(uv, ur, ca, cb);
                 if (t < gerr) {
                     e = t;
                     o = ln;
@@ -1740,21 +1780,21 @@ __device__ void scalar_endpoints_wave(float ramp[2], const float vals_sorted[16]
 }
 
 // encode_bc4 with the endpoint searches spread over the wave; every lane holds
-// v[] and returns the block.  uv / ur: 16 floats of LDS each, the wave's own.
-__device__ uint64_t encode_bc4_wave(const float v[16], float *uv, float *ur)
+// v[] and returns the block.
+__device__ __forceinline__ uint64_t encode_bc4_wave(const float v[16])
 {
     float s[16];
     bc4_sort(v, s);
     uint8_t ep8[2], ep6[2];
     uint64_t i8, i6 = 0;
     float ramp[2];
-    scalar_endpoints_wave<8, false>(ramp, s, uv, ur);
+    scalar_endpoints_wave<8, false>(ramp, s);
     const float e8 = scalar_cluster<8, false>(v, ramp, i8);
     ep8[0] = (uint8_t)ramp[0];
     ep8[1] = (uint8_t)ramp[1];
     float e6 = 3.402823466e+38f;
     if (!(e8 == 0.f)) {
-        scalar_endpoints_wave<6, true>(ramp, s, uv, ur);
+        scalar_endpoints_wave<6, true>(ramp, s);
         e6 = scalar_cluster<6, true>(v, ramp, i6);
         ep6[0] = (uint8_t)ramp[0];
         ep6[1] = (uint8_t)ramp[1];
@@ -1958,7 +1998,6 @@ __global__ void __launch_bounds__(128) bc1_blocks_wave_kernel(const float *__res
 __global__ void __launch_bounds__(128) bc23_blocks_wave_kernel(const float *__restrict__ blocks, uint32_t n, int fmt,
                                                                Bc1Params p, uint4 *__restrict__ dst)
 {
-    __shared__ float uv[16], ur[16];
     __shared__ uint2 res[2];
     const uint32_t id = blockIdx.x;
     if (id >= n) return;
@@ -1972,7 +2011,7 @@ __global__ void __launch_bounds__(128) bc23_blocks_wave_kernel(const float *__re
 #pragma unroll
         for (int i = 0; i < 16; ++i) v[i] = blk[i * 4 + 3];
         if (fmt == 3) {
-            const uint64_t r = bcx::encode_bc4_wave(v, uv, ur);
+            const uint64_t r = bcx::encode_bc4_wave(v);
             r2 = make_uint2((uint32_t)r, (uint32_t)(r >> 32));
         } else {
             r2 = bcx::encode_explicit_alpha_f32(v);
@@ -1992,13 +2031,12 @@ __global__ void __launch_bounds__(128) bc23_blocks_wave_kernel(const float *__re
 __global__ void __launch_bounds__(64) bc4_blocks_wave_kernel(const float *__restrict__ blocks, uint32_t n,
                                                              uint64_t *__restrict__ dst)
 {
-    __shared__ float uv[16], ur[16];
     const uint32_t id = blockIdx.x;
     if (id >= n) return;
     float v[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = blocks[(size_t)id * 16 + i];
-    const uint64_t b = bcx::encode_bc4_wave(v, uv, ur);
+    const uint64_t b = bcx::encode_bc4_wave(v);
     if (threadIdx.x == 0) dst[id] = b;
 }
 
