@@ -969,6 +969,83 @@ __device__ __forceinline__ void unique_colours(ColF &u, const float in[64], bool
     }
 }
 
+// unique_colours for the one-wave block kernels: every lane holds the block (its
+// 64 floats are wave-uniform), lane i < 16 ranks texel i against the others
+// (16 comparisons instead of every lane running all 256), each leader stores
+// its colour at its unique index in the wave's 64-float LDS row, and every lane
+// reads the row back.  The keys, counts and ranks are the ones unique_colours
+// computes, so ColF is identical.  (All lanes running the 16 x 16 comparisons on
+// wave-uniform values took half of a BC1 block call: ~87 K cycles.)
+__device__ __forceinline__ void unique_colours_wave(ColF &u, const float in[64], bool use_alpha, float thr01, int &kept,
+                                                    float *row)
+{
+    const int L = (int)(threadIdx.x & 63u);
+    bool live[16];
+    kept = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        live[i] = !use_alpha || (in[i * 4 + 3] >= thr01);
+        kept += live[i] ? 1 : 0;
+    }
+    // this lane's texel (lanes >= 16: texel 15, unused)
+    uint32_t k0 = 0, k1 = 0, k2 = 0;
+    bool mylive = false;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        const bool me = (L == t) || (t == 15 && L > 15);
+        k0 = me ? __float_as_uint(in[t * 4 + 2]) : k0;   // B
+        k1 = me ? __float_as_uint(in[t * 4 + 1]) : k1;   // G
+        k2 = me ? __float_as_uint(in[t * 4 + 0]) : k2;   // R
+        mylive = me ? live[t] : mylive;
+    }
+    int less = 0, same_before = 0, same = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        if (!live[j]) continue;   // uniform
+        const uint32_t j0 = __float_as_uint(in[j * 4 + 2]), j1 = __float_as_uint(in[j * 4 + 1]),
+                       j2 = __float_as_uint(in[j * 4 + 0]);
+        const bool eq = j0 == k0 && j1 == k1 && j2 == k2;
+        const bool lt = j2 < k2 || (j2 == k2 && (j1 < k1 || (j1 == k1 && j0 < k0)));
+        same += eq ? 1 : 0;
+        same_before += (eq && j < L) ? 1 : 0;
+        less += lt ? 1 : 0;
+    }
+    const bool lead = L < 16 && mylive && same_before == 0;
+    const uint64_t lm = __ballot(lead);
+    u.n = __popcll(lm);
+    // unique index = leaders with a smaller rank (ranks of leaders are distinct)
+    int ui = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int rj = __builtin_amdgcn_readlane(less, j);
+        ui += (((lm >> j) & 1u) && rj < less) ? 1 : 0;
+    }
+    if (lead) {
+        float mine[4];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            float v = 0.f;
+#pragma unroll
+            for (int t = 0; t < 16; ++t) v = (L == t) ? in[t * 4 + 2 - c] : v;
+            mine[c] = (float)((double)v * 255.0);
+        }
+        mine[3] = (float)same;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) row[ui * 4 + c] = mine[c];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const bool in_k = k < u.n;
+        u.cc[k][0] = in_k ? row[k * 4 + 0] : 0.f;
+        u.cc[k][1] = in_k ? row[k * 4 + 1] : 0.f;
+        u.cc[k][2] = in_k ? row[k * 4 + 2] : 0.f;
+        u.r[k] = in_k ? row[k * 4 + 3] : 0.f;
+    }
+}
+
 // Texel access for the final clustering: R, G, B as in * 255.0f and the
 // alpha test !(A * 255 >= thr * 255).
 struct TexB {
@@ -1960,6 +2037,7 @@ __global__ void __launch_bounds__(128) bc1_blocks_wave_kernel(const float *__res
 {
     __shared__ uint2 res[2];
     __shared__ float err[2];
+    __shared__ float ucol[2][64];
     const uint32_t id = blockIdx.x;
     if (id >= n) return;
     float blk[64];
@@ -1969,7 +2047,7 @@ __global__ void __launch_bounds__(128) bc1_blocks_wave_kernel(const float *__res
     const bool use_alpha = thr01 > 0.0f;
     bcx::ColF u;
     int kept;
-    bcx::unique_colours(u, blk, use_alpha, thr01, kept);
+    bcx::unique_colours_wave(u, blk, use_alpha, thr01, kept, ucol[threadIdx.x >> 6]);
     const bcx::TexF t{blk, thr01 * 255.f};
     const int w = (int)(threadIdx.x >> 6);
     uint8_t ep[3][2];
@@ -1999,6 +2077,7 @@ __global__ void __launch_bounds__(128) bc23_blocks_wave_kernel(const float *__re
                                                                Bc1Params p, uint4 *__restrict__ dst)
 {
     __shared__ uint2 res[2];
+    __shared__ float ucol[64];
     const uint32_t id = blockIdx.x;
     if (id >= n) return;
     float blk[64];
@@ -2019,7 +2098,7 @@ __global__ void __launch_bounds__(128) bc23_blocks_wave_kernel(const float *__re
     } else {
         bcx::ColF u;
         int kept;
-        bcx::unique_colours(u, blk, false, 0.f, kept);
+        bcx::unique_colours_wave(u, blk, false, 0.f, kept, ucol);
         const bcx::TexF t{blk, 0.f};
         r2 = bcx::encode_rgb4<false, true>(u, kept, t, p.steps);
     }
