@@ -183,7 +183,25 @@ __device__ __forceinline__ uint64_t nibble_mask(uint32_t m)
 // a problem's result is updated only if want[s] (find_optimal_solution's
 // changed-endpoints test).  Texels outside a K = 1 problem's mask are computed
 // and discarded (branch-free); the integer totals do not depend on order.
-template <bool P, int K, class Y = Ycc>
+// bit i of m (i < 16) to bit 4i (the selector nibbles' bit 0)
+__device__ __forceinline__ uint64_t spread4(uint32_t m)
+{
+    uint64_t x = m & 0xffffu;
+    x = (x | (x << 24)) & 0x000000ff000000ffull;
+    x = (x | (x << 12)) & 0x000f000f000f000full;
+    x = (x | (x << 6)) & 0x0303030303030303ull;
+    x = (x | (x << 3)) & 0x1111111111111111ull;
+    return x;
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+    return v;
+}
+
+template <bool P, int K, class Y = Ycc, bool WAVE = false>
 __device__ __forceinline__ void evaluate(const uint32_t lo[K], const uint32_t hi[K], const uint32_t pb0[K],
                                          const uint32_t pb1[K], const bool want[K], const Prob pr[K], uint32_t m0,
                                          const uint32_t px[16], const Y &tx, const EncCfg &cf, Res r[K])
@@ -252,6 +270,40 @@ __device__ __forceinline__ void evaluate(const uint32_t lo[K], const uint32_t hi
             if (K == 2) tot[K - 1] += f0 ? 0u : e;
             ts |= (uint64_t)(in ? (uint32_t)(sl - down) : 0u) << (4 * i);
         }
+    } else if constexpr (WAVE) {
+        // one block per wave (every lane holds it): lane L scores texel L & 15
+        // against ramp points L >> 4, + 4, ... and the four lanes of a texel take
+        // the minimum of (error << 4 | selector) -- the same minimum as the
+        // sequential scan below (min is order-free; errors are < 2^28); the
+        // subset totals are integer sums, the selectors gathered by ballots.
+        const int L = (int)(threadIdx.x & 63u);
+        const int i = L & 15;
+        const bool f0 = first_subset<K>(m0, i);
+        const uint32_t A = f0 ? a[0] : a[K - 1], B = f0 ? b[0] : b[K - 1];
+        uint32_t c = px[0];
+#pragma unroll
+        for (int t = 1; t < 16; ++t) c = i == t ? px[t] : c;
+        const int tl = tx.l(i), tcr = tx.cr(i), tcb = tx.cb(i);
+        uint32_t key = kNone;
+        for (uint32_t j = (uint32_t)(L >> 4); j < N; j += 4) {
+            const uint32_t w = bc7w(j, N);
+            int l1, cr1, cb1;
+            ycc(lerp_ch(A, B, 0, w), lerp_ch(A, B, 1, w), lerp_ch(A, B, 2, w), l1, cr1, cb1);
+            int ea = 0;
+            if (any_alpha) {   // wave-uniform; K == 1
+                const int d = lerp_ch(A, B, 3, w) - (int)ch(c, 3);
+                ea = mad24(mul24(w3, d), d, 0);
+            }
+            key = min(key, (ycc_err(l1, cr1, cb1, tl, tcr, tcb, cf, ea) << 4) | j);
+        }
+        key = min(key, (uint32_t)__shfl_xor((int)key, 16));
+        key = min(key, (uint32_t)__shfl_xor((int)key, 32));
+        const bool in = L < 16 && ((mask >> i) & 1u);
+        tot[0] = wave_sum_u32((in && f0) ? key >> 4 : 0u);
+        if (K == 2) tot[K - 1] = wave_sum_u32((L < 16 && !f0) ? key >> 4 : 0u);
+        const uint32_t sl = in ? key & 15u : 0u;
+#pragma unroll
+        for (int bit = 0; bit < 4; ++bit) ts |= spread4((uint32_t)__ballot((sl >> bit) & 1u)) << bit;
     } else {
         // ramp point outer (a real loop), texels inner.  Each texel keeps the
         // minimum of (error << 4 | selector): the least error, first selector on
@@ -388,7 +440,7 @@ __device__ __forceinline__ void quantize(float xl[4], float xh[4], const Prob &p
 
 // find_optimal_solution for the K problems: quantise each active one's
 // endpoints, evaluate those that differ from its best (:710, :724)
-template <bool P, int K, class Y = Ycc>
+template <bool P, int K, class Y = Ycc, bool WAVE = false>
 __device__ __forceinline__ void fit(float xl[K][4], float xh[K][4], const bool active[K], const Prob pr[K],
                                     uint32_t m0, const uint32_t px[16], const Y &tx, const EncCfg &cf, Res r[K])
 {
@@ -401,7 +453,7 @@ __device__ __forceinline__ void fit(float xl[K][4], float xh[K][4], const bool a
                                 p1[s] != r[s].pb1);
         any = any || want[s];
     }
-    if (any) evaluate<P, K>(lo, hi, p0, p1, want, pr, m0, px, tx, cf, r);
+    if (any) evaluate<P, K, Y, WAVE>(lo, hi, p0, p1, want, pr, m0, px, tx, cf, r);
 }
 
 // compute_least_squares_endpoints_rgb / _rgba :197-280 for the K problems in
@@ -618,7 +670,7 @@ __device__ __forceinline__ void pca_endpoints(const Prob &pr, const uint32_t px[
 }
 
 // color_cell_compression :731-1024 for K problems in lockstep
-template <bool P, int K, class Y = Ycc>
+template <bool P, int K, class Y = Ycc, bool WAVE = false>
 __device__ __forceinline__ void cells(const Prob pr[K], uint32_t m0, const uint32_t px[16], const Y &tx,
                                       const EncCfg &cf, const EncLds &L, Res r[K])
 {
@@ -725,7 +777,7 @@ __device__ __forceinline__ void cells(const Prob pr[K], uint32_t m0, const uint3
             }
             lsq<K>(pr, m0, ts, px, L, xl, xh);
         }
-        fit<P, K>(xl, xh, active, pr, m0, px, tx, cf, r);
+        fit<P, K, Y, WAVE>(xl, xh, active, pr, m0, px, tx, cf, r);
 #pragma unroll
         for (int s = 0; s < K; ++s) zero[s] = zero[s] || (active[s] && r[s].err == 0);
     }
@@ -976,7 +1028,7 @@ __device__ __forceinline__ uint4 encode_block(const uint32_t px[16], const EncCf
     {   // mode 6 on the whole block
         Prob p6[1];
         p6[0].mask = 0xffffu, p6[0].n = 16, p6[0].nsel = 16, p6[0].cbits = 7, p6[0].mode1 = false, p6[0].alpha = alpha;
-        cells<P, 1>(p6, 0xffffu, px, tx, cf, L, r6);
+        cells<P, 1, Y, WAVE>(p6, 0xffffu, px, tx, cf, L, r6);
     }
     if (!alpha && r6[0].err > 0 && cf.max_parts > 0) {
         // mode 1 on the partition the estimator picks, both subsets at once (the
@@ -990,7 +1042,7 @@ __device__ __forceinline__ uint4 encode_block(const uint32_t px[16], const EncCf
             p1[k].n = (uint32_t)__popc(p1[k].mask), p1[k].nsel = 8, p1[k].cbits = 6, p1[k].mode1 = true;
             p1[k].alpha = false;
         }
-        cells<P, 2>(p1, m0, px, tx, cf, L, r1);
+        cells<P, 2, Y, WAVE>(p1, m0, px, tx, cf, L, r1);
         mode1 = r1[0].err + r1[1].err < r6[0].err;
     }
     const Res s0 = r1[0], s1 = r1[1];
