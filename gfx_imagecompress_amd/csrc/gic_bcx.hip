@@ -185,8 +185,16 @@ struct ColLT {
         return r;
     }
 };
+// ColF with FindAxis' inputs cc / 255.f divided once (the one-wave block kernels:
+// the divisions recomputed in every axis iteration's projection and direction
+// loops were a quarter of a BC1 block's search)
+struct ColFW : ColF {
+    float bk[16][3];
+    __device__ __forceinline__ float blk(int i, int ch) const { return bk[i][ch]; }
+};
 __device__ __forceinline__ const ColB &regs(const ColB &u) { return u; }
 __device__ __forceinline__ const ColF &regs(const ColF &u) { return u; }
+__device__ __forceinline__ const ColFW &regs(const ColFW &u) { return u; }
 template <bool S1>
 __device__ __forceinline__ ColB regs(const ColLT<S1> &u) { return u.regs(); }
 
@@ -976,7 +984,7 @@ __device__ __forceinline__ void unique_colours(ColF &u, const float in[64], bool
 // reads the row back.  The keys, counts and ranks are the ones unique_colours
 // computes, so ColF is identical.  (All lanes running the 16 x 16 comparisons on
 // wave-uniform values took half of a BC1 block call: ~87 K cycles.)
-__device__ __forceinline__ void unique_colours_wave(ColF &u, const float in[64], bool use_alpha, float thr01, int &kept,
+__device__ __forceinline__ void unique_colours_wave(ColFW &u, const float in[64], bool use_alpha, float thr01, int &kept,
                                                     float *row)
 {
     const int L = (int)(threadIdx.x & 63u);
@@ -1043,6 +1051,8 @@ __device__ __forceinline__ void unique_colours_wave(ColF &u, const float in[64],
         u.cc[k][1] = in_k ? row[k * 4 + 1] : 0.f;
         u.cc[k][2] = in_k ? row[k * 4 + 2] : 0.f;
         u.r[k] = in_k ? row[k * 4 + 3] : 0.f;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) u.bk[k][c] = u.cc[k][c] / 255.f;
     }
 }
 
@@ -2045,7 +2055,7 @@ __global__ void __launch_bounds__(128) bc1_blocks_wave_kernel(const float *__res
     for (int i = 0; i < 64; ++i) blk[i] = blocks[(size_t)id * 64 + i];
     const float thr01 = p.alpha_threshold;
     const bool use_alpha = thr01 > 0.0f;
-    bcx::ColF u;
+    bcx::ColFW u;
     int kept;
     bcx::unique_colours_wave(u, blk, use_alpha, thr01, kept, ucol[threadIdx.x >> 6]);
     const bcx::TexF t{blk, thr01 * 255.f};
@@ -2096,7 +2106,7 @@ __global__ void __launch_bounds__(128) bc23_blocks_wave_kernel(const float *__re
             r2 = bcx::encode_explicit_alpha_f32(v);
         }
     } else {
-        bcx::ColF u;
+        bcx::ColFW u;
         int kept;
         bcx::unique_colours_wave(u, blk, false, 0.f, kept, ucol);
         const bcx::TexF t{blk, 0.f};
