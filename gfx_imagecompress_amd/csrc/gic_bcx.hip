@@ -229,17 +229,37 @@ __device__ __forceinline__ float ramp_fit_error(const Col &u, const float r[3][4
 
 // (e, order) of the lane with the smallest e, ties to the smallest order; a lane
 // without a candidate brings e = +inf
+// Unsigned minimum over the wave: DPP inside each 16-lane row (quad_perm xor 1,
+// xor 2, row_ror 4, 8), then the four rows' results by readlane.  The whole
+// wave must be active (every call site is wave-uniform).
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_u(unsigned v)
+{
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ unsigned wave_minu(unsigned v)
+{
+    v = min(v, dpp_u<0xB1>(v));
+    v = min(v, dpp_u<0x4E>(v));
+    v = min(v, dpp_u<0x124>(v));
+    v = min(v, dpp_u<0x128>(v));
+    const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)v, 0), b = (unsigned)__builtin_amdgcn_readlane((int)v, 16),
+                   c = (unsigned)__builtin_amdgcn_readlane((int)v, 32), d = (unsigned)__builtin_amdgcn_readlane((int)v, 48);
+    return min(min(a, b), min(c, d));
+}
+
+// (e, o) lexicographic minimum over the wave, on every lane.  Every caller feeds
+// a non-negative, non-NaN e (+inf for "no candidate": the NaN-rejecting tests sit
+// before the call) and o >= 0, so float order is the bit patterns' unsigned
+// order and the minimum does not depend on the reduction order: two DPP
+// minima instead of six rounds of two ds_bpermute shuffles.
 __device__ __forceinline__ void wave_argmin(float &e, int &o)
 {
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1) {
-        const float e2 = __shfl_xor(e, m);
-        const int o2 = __shfl_xor(o, m);
-        if (e2 < e || (e2 == e && o2 < o)) {
-            e = e2;
-            o = o2;
-        }
-    }
+    const unsigned eb = __float_as_uint(e);
+    const unsigned emin = wave_minu(eb);
+    const unsigned om = wave_minu(eb == emin ? (unsigned)o : 0xffffffffu);
+    e = __uint_as_float(emin);
+    o = (int)om;
 }
 
 // Refine, amd_bcx_body.cpp:582-806 (R, then G, then B 3x3 jitter of both
