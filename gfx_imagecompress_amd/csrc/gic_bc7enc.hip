@@ -931,7 +931,7 @@ __device__ __forceinline__ uint32_t pick_partition_wave(const uint32_t px[16], c
             if (it == 34) stop = true;
             continue;
         }
-        const uint32_t e = (uint32_t)__shfl((int)el, (int)it);
+        const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)el, (int)it);   // it: wave-uniform
         if (e < best) best = e, best_part = part;
         if (part == 34 && best_part != 34) stop = true;
         if (it == 13) key = best_part;

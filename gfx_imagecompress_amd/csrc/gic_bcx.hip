@@ -787,8 +787,8 @@ __device__ __forceinline__ void fit_endpoints(float result[3][2], const Col &u, 
                 wave_argmin(e, o);
                 if (o != 0x7fffffff) {
                     err = e;
-                    pos0 = __shfl(lp, o);
-                    pos1 = __shfl(hp, o);
+                    pos0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lp), o));   // o: wave-uniform
+                    pos1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hp), o));
                 }
             } else {
             // entries past 8 that any lane of the wave still has (uniform)
@@ -1869,8 +1869,8 @@ __device__ __forceinline__ void scalar_endpoints_wave(float ramp[2], const float
             }
             wave_argmin(e, o);
             if (o == 0x7fffffff) break;
-            lr = __shfl(ca, o);
-            hr = __shfl(cb, o);
+            lr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ca), o));   // o: wave-uniform
+            hr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cb), o));
             gerr = e;
         }
         lo = lr * 255.f;
