@@ -1673,6 +1673,34 @@ __device__ __forceinline__ void bc4_sort(const float v[16], float s[16])
     }
 }
 
+// bc4_sort for the one-wave kernels: lane i < 16 ranks texel i (16 comparisons
+// instead of every lane computing all 256) and stores it at its rank in the
+// wave's 16-float LDS row; every lane reads the row back.  NaN blocks take the
+// register sort (uniform branch).
+__device__ __forceinline__ void bc4_sort_wave(const float v[16], float s[16], float *row)
+{
+    bool nan = false;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) nan = nan || v[i] != v[i];
+    if (nan) {
+        bc4_sort(v, s);
+        return;
+    }
+    const int L = (int)(threadIdx.x & 63u);
+    float vi = v[0];
+#pragma unroll
+    for (int t = 1; t < 16; ++t) vi = L == t ? v[t] : vi;
+    int r = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) r += (v[j] < vi || (v[j] == vi && j < L)) ? 1 : 0;
+    if (L < 16) row[r] = vi;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s[k] = row[k];
+}
+
 template <class W = Bc4Scratch>
 __device__ uint64_t encode_bc4(const float v[16], W wk = W())
 {
@@ -1823,11 +1851,24 @@ __device__ __forceinline__ void scalar_endpoints_wave(float ramp[2], const float
             for (float sr = rrb; rlb <= sr; sr -= 0.018f) ++nr;
             float be = __builtin_huge_valf();
             int bo = 0x7fffffff;
+            // the loops' endpoint sequences once (the same repeated float steps;
+            // at most 0.2 / 0.018 + 1 = 12 of each), picked per lane
+            float SL[16], SR[16];
+            SL[0] = llb;
+            SR[0] = rrb;
+#pragma unroll
+            for (int k = 1; k < 16; ++k) {
+                SL[k] = SL[k - 1] + 0.018f;
+                SR[k] = SR[k - 1] - 0.018f;
+            }
             for (int t = ln; t < nl * nr; t += 64) {
                 const int i = t / nr, j = t - i * nr;
-                float sl = llb, sr = rrb;
-                for (int k = 0; k < i; ++k) sl += 0.018f;
-                for (int k = 0; k < j; ++k) sr -= 0.018f;
+                float sl = SL[0], sr = SR[0];
+#pragma unroll
+                for (int k = 1; k < 16; ++k) {
+                    sl = k == i ? SL[k] : sl;
+                    sr = k == j ? SR[k] : sr;
+                }
                 const float e = scalar_ramp_error_reg<N>(uv, ur, sl, sr);
                 if (e < 128000.f && e < be) {   // first strictly smaller, per lane in loop order
                     be = e;
@@ -1838,10 +1879,13 @@ __device__ __forceinline__ void scalar_endpoints_wave(float ramp[2], const float
             float gl = 0.f, gr = 0.f;
             if (bo != 0x7fffffff) {
                 const int i = bo / nr, j = bo - i * nr;
-                gl = llb;
-                gr = rrb;
-                for (int k = 0; k < i; ++k) gl += 0.018f;
-                for (int k = 0; k < j; ++k) gr -= 0.018f;
+                gl = SL[0];
+                gr = SR[0];
+#pragma unroll
+                for (int k = 1; k < 16; ++k) {
+                    gl = k == i ? SL[k] : gl;
+                    gr = k == j ? SR[k] : gr;
+                }
                 gerr = be;
             }
             lr = gl;
@@ -1887,11 +1931,11 @@ __device__ __forceinline__ void scalar_endpoints_wave(float ramp[2], const float
 }
 
 // encode_bc4 with the endpoint searches spread over the wave; every lane holds
-// v[] and returns the block.
-__device__ __forceinline__ uint64_t encode_bc4_wave(const float v[16])
+// v[] and returns the block.  row: 16 floats of LDS, the wave's own.
+__device__ __forceinline__ uint64_t encode_bc4_wave(const float v[16], float *row)
 {
     float s[16];
-    bc4_sort(v, s);
+    bc4_sort_wave(v, s, row);
     uint8_t ep8[2], ep6[2];
     uint64_t i8, i6 = 0;
     float ramp[2];
@@ -2107,7 +2151,7 @@ __global__ void __launch_bounds__(128) bc23_blocks_wave_kernel(const float *__re
                                                                Bc1Params p, uint4 *__restrict__ dst)
 {
     __shared__ uint2 res[2];
-    __shared__ float ucol[64];
+    __shared__ float ucol[64], arow[16];
     const uint32_t id = blockIdx.x;
     if (id >= n) return;
     float blk[64];
@@ -2120,7 +2164,7 @@ __global__ void __launch_bounds__(128) bc23_blocks_wave_kernel(const float *__re
 #pragma unroll
         for (int i = 0; i < 16; ++i) v[i] = blk[i * 4 + 3];
         if (fmt == 3) {
-            const uint64_t r = bcx::encode_bc4_wave(v);
+            const uint64_t r = bcx::encode_bc4_wave(v, arow);
             r2 = make_uint2((uint32_t)r, (uint32_t)(r >> 32));
         } else {
             r2 = bcx::encode_explicit_alpha_f32(v);
@@ -2140,12 +2184,13 @@ __global__ void __launch_bounds__(128) bc23_blocks_wave_kernel(const float *__re
 __global__ void __launch_bounds__(64) bc4_blocks_wave_kernel(const float *__restrict__ blocks, uint32_t n,
                                                              uint64_t *__restrict__ dst)
 {
+    __shared__ float srow[16];
     const uint32_t id = blockIdx.x;
     if (id >= n) return;
     float v[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = blocks[(size_t)id * 16 + i];
-    const uint64_t b = bcx::encode_bc4_wave(v);
+    const uint64_t b = bcx::encode_bc4_wave(v, srow);
     if (threadIdx.x == 0) dst[id] = b;
 }
 
