@@ -774,9 +774,19 @@ __device__ __forceinline__ void fit_endpoints(float result[3][2], const Col &u, 
             if constexpr (WAVE) {
                 // candidate (l, h) on lane 8 l + h
                 const int ln = (int)(threadIdx.x & 63u);
+                // the loop's endpoint sequences once (the same repeated float
+                // steps), picked per lane -- per-lane step loops diverge
                 float lp = ls, hp = he;
-                for (int k = 0; k < (ln >> 3); ++k) lp += stp;
-                for (int k = 0; k < (ln & 7); ++k) hp -= stp;
+                {
+                    float a = ls, b = he;
+#pragma unroll
+                    for (int k = 1; k < 8; ++k) {
+                        a += stp;
+                        b -= stp;
+                        lp = (ln >> 3) == k ? a : lp;
+                        hp = (ln & 7) == k ? b : hp;
+                    }
+                }
                 const RampStep rs = ramp_step<N>(lp, hp);
                 float e = proj_ramp_error<8, 16>(proj_ramp_error<0, 8>(0.f, prj, perr, prem, rs), prj, perr, prem, rs);
                 int o = ln;
@@ -1000,7 +1010,7 @@ __device__ __forceinline__ void unique_colours(ColF &u, const float in[64], bool
 // unique_colours for the one-wave block kernels: every lane holds the block (its
 // 64 floats are wave-uniform), lane i < 16 ranks texel i against the others
 // (16 comparisons instead of every lane running all 256), each leader stores
-// its colour at its unique index in the wave's 64-float LDS row, and every lane
+// its colour at its unique index in the wave's 128-float LDS row, and every lane
 // reads the row back.  The keys, counts and ranks are the ones unique_colours
 // computes, so ColF is identical.  (All lanes running the 16 x 16 comparisons on
 // wave-uniform values took half of a BC1 block call: ~87 K cycles.)
@@ -1049,17 +1059,19 @@ __device__ __forceinline__ void unique_colours_wave(ColFW &u, const float in[64]
         ui += (((lm >> j) & 1u) && rj < less) ? 1 : 0;
     }
     if (lead) {
-        float mine[4];
+        float mine[8];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             float v = 0.f;
 #pragma unroll
             for (int t = 0; t < 16; ++t) v = (L == t) ? in[t * 4 + 2 - c] : v;
             mine[c] = (float)((double)v * 255.0);
+            mine[4 + c] = mine[c] / 255.f;   // FindAxis' input, divided by the lane that owns it
         }
         mine[3] = (float)same;
+        mine[7] = 0.f;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) row[ui * 4 + c] = mine[c];
+        for (int c = 0; c < 8; ++c) row[ui * 8 + c] = mine[c];
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1067,12 +1079,12 @@ __device__ __forceinline__ void unique_colours_wave(ColFW &u, const float in[64]
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const bool in_k = k < u.n;
-        u.cc[k][0] = in_k ? row[k * 4 + 0] : 0.f;
-        u.cc[k][1] = in_k ? row[k * 4 + 1] : 0.f;
-        u.cc[k][2] = in_k ? row[k * 4 + 2] : 0.f;
-        u.r[k] = in_k ? row[k * 4 + 3] : 0.f;
+        u.cc[k][0] = in_k ? row[k * 8 + 0] : 0.f;
+        u.cc[k][1] = in_k ? row[k * 8 + 1] : 0.f;
+        u.cc[k][2] = in_k ? row[k * 8 + 2] : 0.f;
+        u.r[k] = in_k ? row[k * 8 + 3] : 0.f;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) u.bk[k][c] = u.cc[k][c] / 255.f;
+        for (int c = 0; c < 3; ++c) u.bk[k][c] = in_k ? row[k * 8 + 4 + c] : 0.f;
     }
 }
 
@@ -2111,7 +2123,7 @@ __global__ void __launch_bounds__(128) bc1_blocks_wave_kernel(const float *__res
 {
     __shared__ uint2 res[2];
     __shared__ float err[2];
-    __shared__ float ucol[2][64];
+    __shared__ float ucol[2][128];
     const uint32_t id = blockIdx.x;
     if (id >= n) return;
     float blk[64];
@@ -2151,7 +2163,7 @@ __global__ void __launch_bounds__(128) bc23_blocks_wave_kernel(const float *__re
                                                                Bc1Params p, uint4 *__restrict__ dst)
 {
     __shared__ uint2 res[2];
-    __shared__ float ucol[64], arow[16];
+    __shared__ float ucol[128], arow[16];
     const uint32_t id = blockIdx.x;
     if (id >= n) return;
     float blk[64];
