@@ -187,10 +187,16 @@ class Split:
 
 class RootGather:
     """The rank's encode target (padded to the largest shard) and one gather of
-    it to rank 0 -- torch.distributed.gather into preallocated views of one
-    buffer: RCCL's grouped send/recv over xGMI on device tensors, gloo on host
-    copies in the rehearsal.  With contiguous equal shards the root's buffer is
-    already the image in reference block order."""
+    it to rank 0 per step -- torch.distributed.gather into preallocated views of
+    one buffer: RCCL's grouped send/recv over xGMI on device tensors, gloo on
+    host copies in the rehearsal.  With contiguous equal shards the root's
+    buffer is already the image in reference block order.
+
+    Two encode targets alternate over the steps and each gather is issued
+    asynchronously, so step k + 1's encode overlaps step k's gather: before an
+    encode writes a target, `local` waits for the gather that last read it
+    (RCCL: the encode stream waits on the collective, the host does not), and
+    drain() waits for the rest before the timed region's closing sync."""
 
     def __init__(self, split, bx, bb, dev):
         import torch
@@ -199,18 +205,39 @@ class RootGather:
         self.world = split.world
         self.gloo = self.world > 1 and dist.get_backend() == "gloo"
         self.n = split.most * bx * bb
-        self.local = torch.empty(max(1, self.n), dtype=torch.uint8, device=dev)
+        nbuf = 2 if self.world > 1 else 1
+        self.bufs = [torch.empty(max(1, self.n), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+        self.pending = [None] * nbuf
+        self.k = 0      # the target the next encode writes
+        self.last = 0   # the target the last encode wrote
         self.parts = None
         if self.world > 1 and split.rank == 0:
             buf = torch.empty(self.world * self.n, dtype=torch.uint8, device="cpu" if self.gloo else dev)
             self.parts = list(buf.view(self.world, self.n))
 
+    @property
+    def local(self):
+        """The encode target of this step (after the gather that last read it)."""
+        w = self.pending[self.k]
+        if w is not None:
+            w.wait()
+            self.pending[self.k] = None
+        return self.bufs[self.k]
+
     def __call__(self):
         import torch.distributed as dist
         if self.world <= 1:
             return
-        t = self.local.cpu() if self.gloo else self.local
-        dist.gather(t, gather_list=self.parts, dst=0)
+        t = self.bufs[self.k].cpu() if self.gloo else self.bufs[self.k]
+        self.pending[self.k] = dist.gather(t, gather_list=self.parts, dst=0, async_op=True)
+        self.last = self.k
+        self.k ^= 1
+
+    def drain(self):
+        for i, w in enumerate(self.pending):
+            if w is not None:
+                w.wait()
+                self.pending[i] = None
 
     def tail(self):
         """The per-step gather (None for one rank)."""
@@ -220,9 +247,10 @@ class RootGather:
         """Rank 0: the blocks of its texture in reference order as a host
         array (strong: the whole gathered image; weak / one rank: its own)."""
         import torch
+        self.drain()
         rb = self.bx * self.bb
         if self.world == 1 or self.split.weak:
-            return self.local[: self.split.rows * rb].cpu().numpy()
+            return self.bufs[self.last][: self.split.rows * rb].cpu().numpy()
         return torch.cat([self.parts[r][: n * rb] for r, (_, n) in enumerate(self.split.spans)]).cpu().numpy()
 
 
@@ -285,6 +313,8 @@ def _timed(world, dev, stream, fn, steps, tail=None):
         e1.record(stream)
         if tail is not None:
             tail()
+    if tail is not None and hasattr(tail, "drain"):
+        tail.drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

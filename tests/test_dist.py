@@ -185,8 +185,8 @@ def _split_worker(rank, world, port, q):
             g = bench.RootGather(split, bx, 8 if fmt == 1 else 16, "cpu")
             out = oracle_lib.encode_image(fmt, img, bc4_channel=0, first_row=split.first, num_rows=split.rows,
                                           threads=2).reshape(-1)
-            g.local[: out.size] = torch.from_numpy(out)
-            for _ in range(2):      # two timed steps gather twice: idempotent
+            for _ in range(3):      # three timed steps: encode into this step's target, gather it
+                g.local[: out.size] = torch.from_numpy(out)   # (asynchronously; the targets alternate)
                 g()
             res.append((fmt, size, split.first, split.rows, None if rank else g.image_host().tobytes()))
         dist.barrier()
