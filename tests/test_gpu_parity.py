@@ -496,6 +496,14 @@ def test_bc1_bc3_non_finite_float_texels(gpu, kind):
         lib.Image_CompressAMDBC1Block(np.ascontiguousarray(blk).ctypes.data_as(ctypes.c_void_p), False, False, 1,
                                       ctypes.c_float(128 / 255.0), out.ctypes.data_as(ctypes.c_void_p))
         assert out.tobytes() == oracle_lib.bc1_block(blk), (kind, i)
+        # each channel as a BC4 block (the one-wave kernel: lane-parallel sort with
+        # the register sort for NaN blocks, register value table)
+        for c in range(4):
+            v = np.ascontiguousarray(blk.reshape(16, 4)[:, c])
+            out4 = np.zeros(8, np.uint8)
+            lib.Image_CompressAMDAlphaSingleModeBlock(v.ctypes.data_as(ctypes.c_void_p),
+                                                      out4.ctypes.data_as(ctypes.c_void_p))
+            assert out4.tobytes() == oracle_lib.bc4_block(v), (kind, i, c)
     # the same blocks as a 4 x 12-block FLOAT32 image
     tex = blocks.reshape(4, 12, 4, 4, 4).transpose(0, 2, 1, 3, 4).reshape(16, 48, 4)
     src = torch.from_numpy(np.ascontiguousarray(tex)).cuda()
