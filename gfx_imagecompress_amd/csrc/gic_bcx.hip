@@ -190,8 +190,18 @@ struct ColLT {
 // loops were a quarter of a BC1 block's search)
 struct ColFW : ColF {
     float bk[16][3];
+    float *urow;   // the wave's LDS rows: 16 x 8 colour words, then 32 + 64 floats of exchange
     __device__ __forceinline__ float blk(int i, int ch) const { return bk[i][ch]; }
 };
+template <class C> struct LaneRows { static constexpr bool v = false; };
+template <> struct LaneRows<ColFW> { static constexpr bool v = true; };
+
+__device__ __forceinline__ void wave_sync_lds()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 __device__ __forceinline__ const ColB &regs(const ColB &u) { return u; }
 __device__ __forceinline__ const ColF &regs(const ColF &u) { return u; }
 __device__ __forceinline__ const ColFW &regs(const ColFW &u) { return u; }
@@ -278,6 +288,37 @@ __device__ __forceinline__ void refine_pass(float cur[3][2], const float base[3]
 #pragma unroll
         for (int c = 0; c < 3; ++c) chan_ramp<N>(r[c], wk[c]);
     }
+    if constexpr (WAVE && LaneRows<Col>::v) {
+        // one-wave kernels: lane i < n forms colour i's side terms (the same
+        // expressions), the wave reads the table back (entries past n: unused
+        // by the count-0 colours, read as written or stale, multiplied by 0)
+        const int L = (int)(threadIdx.x & 63u);
+        float *y = u.urow + 160;
+        if (L < u.n) {
+            const float c0 = u.urow[L * 8 + 0], c1 = u.urow[L * 8 + 1], c2 = u.urow[L * 8 + 2];
+            const float cc[3] = {c0, c1, c2};
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                float v;
+                if (CH == CH_R) {
+                    float dg = r[CH_G][k] - cc[CH_G], db = r[CH_B][k] - cc[CH_B];
+                    v = dg * dg * wg + db * db * wb;
+                } else if (CH == CH_G) {
+                    float dr = r[CH_R][k] - cc[CH_R], db = r[CH_B][k] - cc[CH_B];
+                    v = dr * dr * wr + db * db * wb;
+                } else {
+                    float dr = r[CH_R][k] - cc[CH_R], dg = r[CH_G][k] - cc[CH_G];
+                    v = dr * dr * wr + dg * dg * wg;
+                }
+                y[L * 4 + k] = v;
+            }
+        }
+        wave_sync_lds();
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+#pragma unroll
+            for (int k = 0; k < N; ++k) side[k][i] = i < u.n ? y[i * 4 + k] : 0.f;
+    } else {
 #pragma unroll
     for (int i = 0; i < 16; ++i)
 #pragma unroll
@@ -293,6 +334,7 @@ __device__ __forceinline__ void refine_pass(float cur[3][2], const float base[3]
                 side[k][i] = dr * dr * wr + dg * dg * wg;
             }
         }
+    }
     const float grid = (float)(1 << (8 - chan_bits(CH)));
     const float wc = (CH == CH_R) ? wr : (CH == CH_G) ? wg : wb;
     float b0 = base[CH][0], b1 = base[CH][1];
@@ -738,6 +780,35 @@ __device__ __forceinline__ void fit_endpoints(float result[3][2], const Col &u, 
         float prj[16], perr[16], prem[16];
         for (;;) {
             float bnd0 = 1000.f, bnd1 = -1000.f;
+            if constexpr (WAVE && LaneRows<Col>::v) {
+                // one-wave kernels: lane i < n projects colour i (the same float
+                // expressions), the wave reads the 32 results back, the bounds
+                // scan runs in colour order as below
+                const int L = (int)(threadIdx.x & 63u);
+                float *x = u.urow + 128;
+                if (L < u.n) {
+                    float sh[3];
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) sh[j] = u.urow[L * 8 + 4 + j] - mid[j];
+                    const float q = sh[0] * dir[0] + sh[1] * dir[1] + sh[2] * dir[2];
+                    const float e = (sh[0] - dir[0] * q) * (sh[0] - dir[0] * q) +
+                                    (sh[1] - dir[1] * q) * (sh[1] - dir[1] * q) +
+                                    (sh[2] - dir[2] * q) * (sh[2] - dir[2] * q);
+                    x[L] = q;
+                    x[16 + L] = e;
+                }
+                wave_sync_lds();
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const bool in = i < u.n;
+                    prj[i] = in ? x[i] : 0.f;
+                    perr[i] = in ? x[16 + i] : 0.f;
+                    if (in) {
+                        bnd0 = minr(bnd0, prj[i]);
+                        bnd1 = maxr(bnd1, prj[i]);
+                    }
+                }
+            } else {
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 float sh[3];
@@ -753,6 +824,7 @@ __device__ __forceinline__ void fit_endpoints(float result[3][2], const Col &u, 
                     bnd0 = minr(bnd0, q);
                     bnd1 = maxr(bnd1, q);
                 }
+            }
             }
             const float scl0 = bnd0 - (bnd1 - bnd0) * 0.125f;
             const float scl1 = bnd1 + (bnd1 - bnd0) * 0.125f;
@@ -838,6 +910,39 @@ __device__ __forceinline__ void fit_endpoints(float result[3][2], const Col &u, 
             const float over_n = 1.f / (float)(N - 1);
             const float avg = (float)(N - 1) / 2.f;
             float crs[3] = {0, 0, 0}, len = 0.f;
+            if constexpr (WAVE && LaneRows<Col>::v) {
+                // lane i < n forms colour i's four products, the sums run in
+                // colour order over the read-back values (the same additions)
+                const int L = (int)(threadIdx.x & 63u);
+                float *y = u.urow + 160;
+                if (L < u.n) {
+                    float sh[3];
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) sh[j] = u.urow[L * 8 + 4 + j] - mid[j];
+                    const float p0 = sh[0] * dir[0] + sh[1] * dir[1] + sh[2] * dir[2];
+                    float ri, del;
+                    if ((del = p0 - pos0) <= 0)
+                        ri = 0.f;
+                    else if (p0 - pos1 >= 0)
+                        ri = (float)(N - 1);
+                    else
+                        ri = floorf((del + step_h) * rstep);
+                    ri = (ri - avg) * over_n;
+                    const float pm = ri * u.urow[L * 8 + 3];
+                    y[L * 4 + 0] = ri * pm;
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) y[L * 4 + 1 + j] = sh[j] * pm;
+                }
+                wave_sync_lds();
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    if (i < u.n) {
+                        len += y[i * 4 + 0];
+#pragma unroll
+                        for (int j = 0; j < 3; ++j) crs[j] += y[i * 4 + 1 + j];
+                    }
+                }
+            } else
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 if (i < u.n) {
@@ -1010,7 +1115,7 @@ __device__ __forceinline__ void unique_colours(ColF &u, const float in[64], bool
 // unique_colours for the one-wave block kernels: every lane holds the block (its
 // 64 floats are wave-uniform), lane i < 16 ranks texel i against the others
 // (16 comparisons instead of every lane running all 256), each leader stores
-// its colour at its unique index in the wave's 128-float LDS row, and every lane
+// its colour at its unique index in the wave's LDS rows (224 floats), and every lane
 // reads the row back.  The keys, counts and ranks are the ones unique_colours
 // computes, so ColF is identical.  (All lanes running the 16 x 16 comparisons on
 // wave-uniform values took half of a BC1 block call: ~87 K cycles.)
@@ -1086,6 +1191,7 @@ __device__ __forceinline__ void unique_colours_wave(ColFW &u, const float in[64]
 #pragma unroll
         for (int c = 0; c < 3; ++c) u.bk[k][c] = in_k ? row[k * 8 + 4 + c] : 0.f;
     }
+    u.urow = row;
 }
 
 // Texel access for the final clustering: R, G, B as in * 255.0f and the
@@ -2123,7 +2229,7 @@ __global__ void __launch_bounds__(128) bc1_blocks_wave_kernel(const float *__res
 {
     __shared__ uint2 res[2];
     __shared__ float err[2];
-    __shared__ float ucol[2][128];
+    __shared__ float ucol[2][224];
     const uint32_t id = blockIdx.x;
     if (id >= n) return;
     float blk[64];
@@ -2163,7 +2269,7 @@ __global__ void __launch_bounds__(128) bc23_blocks_wave_kernel(const float *__re
                                                                Bc1Params p, uint4 *__restrict__ dst)
 {
     __shared__ uint2 res[2];
-    __shared__ float ucol[128], arow[16];
+    __shared__ float ucol[224], arow[16];
     const uint32_t id = blockIdx.x;
     if (id >= n) return;
     float blk[64];
