@@ -1113,6 +1113,9 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
                     if (dup) ST(15, 1); else { sigs[nsig][0] = sig; sigs[nsig++][1] = sig1; }
                 }
 #endif
+#ifdef ORC_STATS
+                int st_walked_ = 0;   /* non-repeated passes of this expansion (slots 17..21) */
+#endif
                 for (int odd = 0; odd <= use_par; ++odd)
                     for (int flip = 0; flip <= bcc; ++flip) {
                         int epi[2][4][2]; ST(3, 1); ST(4, n);
@@ -1136,6 +1139,7 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
                             ST(36, 1);
                             if (dup) ST(37, 1); else if (npsig < 512) psig[npsig++] = ps;
                             st_dup_ = dup;
+                            st_walked_ += !dup;
                         }
                         double te_[64][16];
                         const double thr_ = err1 < err2 ? err1 : err2;
@@ -1243,6 +1247,9 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
                             epo1[1][j] = epi[1][j][(s1 >> (2 * j + 1)) & 1];
                         }
                     }
+#ifdef ORC_STATS
+                ST(17 + (st_walked_ < 4 ? st_walked_ : 4), 1);
+#endif
                 if (err1 < err2) {
                     for (int i = 0; i < n; ++i) idx2[i] = idx1[i];
                     err2 = err1;
