@@ -2794,7 +2794,18 @@ struct DeviceState {
     uint32_t h4_cap = 0;
     uint32_t *h4_cnt = nullptr;
     unsigned long long nonterm_seen = 0;   // g_nonterm at the end of the last call
+    // the call's two counters (H4 marks, g_nonterm) copied by one kernel into
+    // mapped pinned memory the host reads after its final synchronisation --
+    // two synchronous device-to-host copies were ~50 us of a one-block call
+    volatile unsigned long long *h_cnt = nullptr;
+    unsigned long long *d_cnt = nullptr;
 };
+
+__global__ void k_counters(const uint32_t *__restrict__ h4, unsigned long long *__restrict__ out)
+{
+    out[0] = *h4;
+    out[1] = g_nonterm;
+}
 
 // Caller holds its device's lock.  Lanes are drained at the end of every call, so
 // the list can be replaced here.
@@ -2804,6 +2815,19 @@ static hipError_t get_h4(DeviceState &st, uint32_t total)
     if (!st.h4_cnt) {
         e = hipMalloc(&st.h4_cnt, sizeof(uint32_t));
         if (e != hipSuccess) return e;
+    }
+    if (!st.h_cnt) {
+        void *h = nullptr;
+        e = hipHostMalloc(&h, 2 * sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent);
+        if (e != hipSuccess) return e;
+        void *d = nullptr;
+        e = hipHostGetDevicePointer(&d, h, 0);
+        if (e != hipSuccess) {
+            (void)hipHostFree(h);
+            return e;
+        }
+        st.h_cnt = (volatile unsigned long long *)h;
+        st.d_cnt = (unsigned long long *)d;
     }
     const uint32_t want = total < (1u << 20) ? total : (1u << 20);   // more marked blocks: re-run the whole call
     if (st.h4_cap >= want) return hipSuccess;
@@ -3287,10 +3311,19 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
     // encoded again through the general kernels (uncapped, cycle-checked
     // quantiser), so their output is the reference's.  Deciding needs the
     // marked count on the host: a BC7 call returns with its work complete.
-    for (int k = 0; k < nsets && e == hipSuccess; ++k) e = hipStreamSynchronize(st->lane[k]);
-    uint32_t nh = 0;
-    if (e == hipSuccess) e = hipMemcpy(&nh, st->h4_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost);
+    // lane 0 waits for the others, copies both counters to the mapped words, and
+    // one synchronisation covers the whole call
+    for (int k = 1; k < nsets && e == hipSuccess; ++k) {
+        e = hipEventRecord(st->ev_join[k], st->lane[k]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st->lane[0], st->ev_join[k], 0);
+    }
     if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_counters, dim3(1), dim3(1), 0, st->lane[0], st->h4_cnt, st->d_cnt);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(st->lane[0]);
+    if (e != hipSuccess) return e;
+    const uint32_t nh = (uint32_t)st->h_cnt[0];
+    unsigned long long nt_end = st->h_cnt[1];
     if (nh > 0) {
         const uint32_t *rl = nh <= st->h4_cap ? st->h4_list : nullptr;   // overflow: the whole call
         const uint32_t rn = rl ? nh : total;
@@ -3312,14 +3345,11 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
         e = hipStreamSynchronize(st->lane[0]);
         if (e != hipSuccess) return e;
         t_h4_rerun = rn;
-    }
-    {
-        unsigned long long nt = 0;
-        e = hipMemcpyFromSymbol(&nt, HIP_SYMBOL(g_nonterm), sizeof(nt));
+        e = hipMemcpyFromSymbol(&nt_end, HIP_SYMBOL(g_nonterm), sizeof(nt_end));   // the re-run's cycles
         if (e != hipSuccess) return e;
-        t_h4_nonterm = (uint32_t)(nt - st->nonterm_seen);
-        st->nonterm_seen = nt;
     }
+    t_h4_nonterm = (uint32_t)(nt_end - st->nonterm_seen);
+    st->nonterm_seen = nt_end;
     {   // join: the caller's stream waits for the lanes
         for (int k = 0; k < nsets && e == hipSuccess; ++k) {
             e = hipEventRecord(st->ev_join[k], st->lane[k]);
