@@ -2048,29 +2048,31 @@ __device__ __forceinline__ void scalar_endpoints_wave(float ramp[2], const float
     }
 }
 
-// encode_bc4 with the endpoint searches spread over the wave; every lane holds
-// v[] and returns the block.  row: 16 floats of LDS, the wave's own.
-__device__ __forceinline__ uint64_t encode_bc4_wave(const float v[16], float *row)
+// One of encode_bc4's two ramp modes with the endpoint searches spread over the
+// wave (N = 8: the 8-value ramp; N = 6, FIXED: the 6-value ramp with 0 and 255);
+// every lane holds v[] and gets the mode's error and block.  row: 16 floats of
+// LDS, the wave's own.  The block kernels run the two modes on two waves at once
+// and join them with bc4_pick.
+template <int N, bool FIXED>
+__device__ __forceinline__ float encode_bc4_mode_wave(const float v[16], float *row, uint64_t &block)
 {
     float s[16];
     bc4_sort_wave(v, s, row);
-    uint8_t ep8[2], ep6[2];
-    uint64_t i8, i6 = 0;
     float ramp[2];
-    scalar_endpoints_wave<8, false>(ramp, s);
-    const float e8 = scalar_cluster<8, false>(v, ramp, i8);
-    ep8[0] = (uint8_t)ramp[0];
-    ep8[1] = (uint8_t)ramp[1];
-    float e6 = 3.402823466e+38f;
-    if (!(e8 == 0.f)) {
-        scalar_endpoints_wave<6, true>(ramp, s);
-        e6 = scalar_cluster<6, true>(v, ramp, i6);
-        ep6[0] = (uint8_t)ramp[0];
-        ep6[1] = (uint8_t)ramp[1];
-    }
-    const bool use8 = e8 <= e6;
-    const uint8_t *ep = use8 ? ep8 : ep6;
-    return (uint64_t)ep[0] | ((uint64_t)ep[1] << 8) | ((use8 ? i8 : i6) << 16);
+    scalar_endpoints_wave<N, FIXED>(ramp, s);
+    uint64_t ib;
+    const float e = scalar_cluster<N, FIXED>(v, ramp, ib);
+    const uint8_t e0 = (uint8_t)ramp[0], e1 = (uint8_t)ramp[1];
+    block = (uint64_t)e0 | ((uint64_t)e1 << 8) | (ib << 16);
+    return e;
+}
+
+// encode_bc4's choice: the 6-value mode runs only when the 8-value error is not
+// 0 (e6 = FLT_MAX otherwise), then use8 = e8 <= e6.  Computing the 6-value mode
+// unconditionally and choosing this way returns the same block.
+__device__ __forceinline__ uint64_t bc4_pick(float e8, uint64_t b8, float e6, uint64_t b6)
+{
+    return (e8 == 0.f || e8 <= e6) ? b8 : b6;
 }
 
 }  // namespace bcx
@@ -2264,52 +2266,81 @@ __global__ void __launch_bounds__(128) bc1_blocks_wave_kernel(const float *__res
     }
 }
 
-// the same for BC2 / BC3: wave 0 the colour half, wave 1 the alpha half
-__global__ void __launch_bounds__(128) bc23_blocks_wave_kernel(const float *__restrict__ blocks, uint32_t n, int fmt,
+// the same for BC2 / BC3: wave 0 the colour half, wave 1 the alpha half (BC3:
+// waves 1 and 2 the alpha half's 8- and 6-value ramp modes, 192 threads)
+__global__ void __launch_bounds__(192) bc23_blocks_wave_kernel(const float *__restrict__ blocks, uint32_t n, int fmt,
                                                                Bc1Params p, uint4 *__restrict__ dst)
 {
-    __shared__ uint2 res[2];
-    __shared__ float ucol[224], arow[16];
+    __shared__ uint2 res;
+    __shared__ uint64_t ares[2];
+    __shared__ float aerr[2];
+    __shared__ float ucol[224], arow[2][16];
     const uint32_t id = blockIdx.x;
     if (id >= n) return;
     float blk[64];
 #pragma unroll
     for (int i = 0; i < 64; ++i) blk[i] = blocks[(size_t)id * 64 + i];
     const int w = (int)(threadIdx.x >> 6);
-    uint2 r2;
-    if (w == 1) {
+    if (w >= 1) {
         float v[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) v[i] = blk[i * 4 + 3];
+        uint64_t r;
+        float e = 0.f;
         if (fmt == 3) {
-            const uint64_t r = bcx::encode_bc4_wave(v, arow);
-            r2 = make_uint2((uint32_t)r, (uint32_t)(r >> 32));
+            if (w == 1)
+                e = bcx::encode_bc4_mode_wave<8, false>(v, arow[0], r);
+            else
+                e = bcx::encode_bc4_mode_wave<6, true>(v, arow[1], r);
         } else {
-            r2 = bcx::encode_explicit_alpha_f32(v);
+            const uint2 a = bcx::encode_explicit_alpha_f32(v);
+            r = (uint64_t)a.x | ((uint64_t)a.y << 32);
+        }
+        if ((threadIdx.x & 63u) == 0) {
+            ares[w - 1] = r;
+            aerr[w - 1] = e;
         }
     } else {
         bcx::ColFW u;
         int kept;
         bcx::unique_colours_wave(u, blk, false, 0.f, kept, ucol);
         const bcx::TexF t{blk, 0.f};
-        r2 = bcx::encode_rgb4<false, true>(u, kept, t, p.steps);
+        const uint2 r2 = bcx::encode_rgb4<false, true>(u, kept, t, p.steps);
+        if (threadIdx.x == 0) res = r2;
     }
-    if ((threadIdx.x & 63u) == 0) res[w] = r2;
     __syncthreads();
-    if (threadIdx.x == 0) dst[id] = make_uint4(res[1].x, res[1].y, res[0].x, res[0].y);
+    if (threadIdx.x == 0) {
+        const uint64_t a = fmt == 3 ? bcx::bc4_pick(aerr[0], ares[0], aerr[1], ares[1]) : ares[0];
+        dst[id] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), res.x, res.y);
+    }
 }
 
-__global__ void __launch_bounds__(64) bc4_blocks_wave_kernel(const float *__restrict__ blocks, uint32_t n,
-                                                             uint64_t *__restrict__ dst)
+// wave 0 the 8-value ramp mode, wave 1 the 6-value one (encode_bc4's two
+// endpoint searches, one after the other on one wave before round 5's last change)
+__global__ void __launch_bounds__(128) bc4_blocks_wave_kernel(const float *__restrict__ blocks, uint32_t n,
+                                                              uint64_t *__restrict__ dst)
 {
-    __shared__ float srow[16];
+    __shared__ float srow[2][16];
+    __shared__ uint64_t res[2];
+    __shared__ float err[2];
     const uint32_t id = blockIdx.x;
     if (id >= n) return;
     float v[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = blocks[(size_t)id * 16 + i];
-    const uint64_t b = bcx::encode_bc4_wave(v, srow);
-    if (threadIdx.x == 0) dst[id] = b;
+    const int w = (int)(threadIdx.x >> 6);
+    uint64_t b;
+    float e;
+    if (w == 0)
+        e = bcx::encode_bc4_mode_wave<8, false>(v, srow[0], b);
+    else
+        e = bcx::encode_bc4_mode_wave<6, true>(v, srow[1], b);
+    if ((threadIdx.x & 63u) == 0) {
+        res[w] = b;
+        err[w] = e;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) dst[id] = bcx::bc4_pick(err[0], res[0], err[1], res[1]);
 }
 
 template <bool R3D>
@@ -2607,7 +2638,8 @@ hipError_t launch_bc23_blocks(const float *blocks, uint32_t n, int fmt, int step
 {
     const Bc1Params p{0.f, steps, 0, 0u, 0u};
     if (n < kWaveBlocks && !r3d) {
-        hipLaunchKernelGGL(bc23_blocks_wave_kernel, dim3(n), dim3(128), 0, s, blocks, n, fmt, p, (uint4 *)dst);
+        hipLaunchKernelGGL(bc23_blocks_wave_kernel, dim3(n), dim3(fmt == 3 ? 192 : 128), 0, s, blocks, n, fmt, p,
+                           (uint4 *)dst);
         return hipGetLastError();
     }
     const uint32_t wg = 256, grid = (n + wg - 1) / wg;
@@ -2646,7 +2678,7 @@ hipError_t launch_bc1_blocks(const float *blocks, uint32_t n, float thr, int ste
 hipError_t launch_bc4_blocks(const float *blocks, uint32_t n, void *dst, hipStream_t s)
 {
     if (n < kWaveBlocks) {
-        hipLaunchKernelGGL(bc4_blocks_wave_kernel, dim3(n), dim3(64), 0, s, blocks, n, (uint64_t *)dst);
+        hipLaunchKernelGGL(bc4_blocks_wave_kernel, dim3(n), dim3(128), 0, s, blocks, n, (uint64_t *)dst);
         return hipGetLastError();
     }
     const uint32_t wg = 256, grid = (n + wg - 1) / wg;

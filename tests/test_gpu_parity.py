@@ -299,8 +299,9 @@ def test_bc23_images(gpu, fmt):
 @pytest.mark.parametrize("n", [97, 4100])
 def test_bc4_block_batch_f32(gpu, n):
     """Block-level BC4 (the batched Image_CompressAMDAlphaSingleModeBlock): below
-    4096 blocks one wave per block (bc4_blocks_wave_kernel, the grid and climb
-    spread over the lanes), from 4096 one lane per block; both bit-exact vs the
+    4096 blocks two waves per block (bc4_blocks_wave_kernel: the 8- and 6-value
+    ramp modes on one wave each, the grid and climb spread over the lanes), from
+    4096 one lane per block; both bit-exact vs the
     oracle on noise, 8-bit grid values, solid and two-value blocks and blocks at
     the FIXED-mode extremes (0 / 1)."""
     import torch
