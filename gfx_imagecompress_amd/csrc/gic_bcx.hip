@@ -1908,39 +1908,45 @@ __device__ __forceinline__ float scalar_ramp_error_reg(const float uv[16], const
 }
 
 template <int N, bool FIXED>
-__device__ __forceinline__ void scalar_endpoints_wave(float ramp[2], const float vals_sorted[16])
+__device__ __forceinline__ void scalar_endpoints_wave(float ramp[2], const float vals_sorted[16], float *row)
 {
     // compaction, scalar_endpoints' loop restated over runs of equal sorted
     // values: a run starts where a value differs from its predecessor (from
     // -2.f before the first, as the loop's `prev`; a NaN always differs), FIXED
-    // keeps a run only strictly inside (1.5/255, 253.5/255); entry k is the k-th
-    // kept run, its value and length.  (A leading run equal to -2.f is dropped:
-    // the loop's out-of-range ur[-1] increment, undefined in the reference.)
-    float uv[16], ur[16];
-    bool st[16], kp[16];
-    int rk[16];
-    int nu = 0;
-    bool started = false;
+    // keeps a run only strictly inside (1.5/255, 253.5/255) -- one test per run,
+    // as a run's texels are one value; entry k is the k-th kept run, its value
+    // and length.  (A leading run equal to -2.f is dropped: the loop's
+    // out-of-range ur[-1] increment, undefined in the reference.)  Lane i < 16
+    // tests sorted texel i; a kept run's first lane writes its entry to the LDS
+    // row (row[16 + k] value, row[32 + k] length, zeros past the last entry).
+    const int ln = (int)(threadIdx.x & 63u);
+    float x = vals_sorted[0], pv = -2.f;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const float x = vals_sorted[i];
-        st[i] = x != (i == 0 ? -2.f : vals_sorted[i - 1]);
-        started = started || st[i];
-        const bool in = !FIXED || (!((double)x <= 1.5 / 255.) && !((double)x >= 253.5 / 255.));
-        kp[i] = started && in;
-        nu += (st[i] && in) ? 1 : 0;
-        rk[i] = nu - 1;   // the entry of this texel's run (if kept)
+    for (int t = 1; t < 16; ++t) {
+        x = ln == t ? vals_sorted[t] : x;
+        pv = ln == t ? vals_sorted[t - 1] : pv;
     }
+    const bool st = ln < 16 && x != pv;
+    const bool in = !FIXED || (!((double)x <= 1.5 / 255.) && !((double)x >= 253.5 / 255.));
+    const uint64_t runs = __ballot(st), kruns = __ballot(st && in);
+    const int nu = __popcll(kruns);
+    if (ln < 16) {
+        row[16 + ln] = 0.f;
+        row[32 + ln] = 0.f;
+    }
+    if (st && in) {
+        const uint64_t later = runs & ~((2ull << ln) - 1ull);
+        const int next = later ? __builtin_ctzll(later) : 16;
+        const int k = __popcll(kruns & ((1ull << ln) - 1ull));
+        row[16 + k] = x;
+        row[32 + k] = (float)(next - ln);
+    }
+    wave_sync_lds();
+    float uv[16], ur[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        float v = 0.f, c = 0.f;
-#pragma unroll
-        for (int i = k; i < 16; ++i) {
-            v = (st[i] && kp[i] && rk[i] == k) ? vals_sorted[i] : v;
-            c += (kp[i] && rk[i] == k) ? 1.f : 0.f;
-        }
-        uv[k] = v;
-        ur[k] = c;
+        uv[k] = row[16 + k];
+        ur[k] = row[32 + k];
     }
     if (nu <= 2) {
         if (FIXED && nu == 0) {
@@ -1951,7 +1957,6 @@ __device__ __forceinline__ void scalar_endpoints_wave(float ramp[2], const float
             ramp[1] = (nu == 1) ? ramp[0] + 1.f : floorf(uv[1] * 255.f + 0.5f);
         }
     } else {
-        const int ln = (int)(threadIdx.x & 63u);
         float lo = uv[0], hi = uv[0];
 #pragma unroll
         for (int k = 1; k < 16; ++k) hi = (k == nu - 1) ? uv[k] : hi;
@@ -2048,21 +2053,84 @@ __device__ __forceinline__ void scalar_endpoints_wave(float ramp[2], const float
     }
 }
 
+// scalar_cluster with texel i on lane i: the same per-texel search, then every
+// lane sums the errors in texel order and packs the indices from an LDS row
+// (row[48 + i] error, row[64 + i] index).
+template <int N, bool FIXED>
+__device__ __forceinline__ float scalar_cluster_wave(const float v[16], float ramp[2], uint64_t &ibits, float *row)
+{
+    ibits = 0;
+    float err = 0.f;
+    if (ramp[0] == ramp[1]) return err;
+    if ((!FIXED && ramp[0] <= ramp[1]) || (FIXED && ramp[0] > ramp[1])) {
+        const float t = ramp[0];
+        ramp[0] = ramp[1];
+        ramp[1] = t;
+    }
+    constexpr int NP = FIXED ? N + 2 : N;
+    float pts[NP];
+    pts[0] = ramp[0];
+    pts[1] = ramp[1];
+#pragma unroll
+    for (int e = 1; e < N - 1; ++e)
+        pts[e + 1] = (pts[0] * (float)(N - 1 - e) + pts[1] * (float)e) / (float)(N - 1);
+    if (FIXED) {
+        pts[N] = 0.f;
+        pts[N + 1] = 255.f;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) pts[i] = floorf(pts[i] + 0.5f) / 1.f;
+    const float over = 1.f / ((float)(1 << 8) - 1.f);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) pts[i] *= over;
+    const int ln = (int)(threadIdx.x & 63u);
+    float vi = v[0];
+#pragma unroll
+    for (int t = 1; t < 16; ++t) vi = ln == t ? v[t] : vi;
+    float best = 10000000.f;
+    int bi = 0;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        float d = vi - pts[j];
+        d *= d;
+        if (d < best) {
+            best = d;
+            bi = j;
+        }
+    }
+    if (ln < 16) {
+        row[48 + ln] = best;
+        row[64 + ln] = (float)bi;
+    }
+    wave_sync_lds();
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        err += row[48 + i];
+        ibits |= (uint64_t)(int)row[64 + i] << (3 * i);
+    }
+    return err;
+}
+
 // One of encode_bc4's two ramp modes with the endpoint searches spread over the
 // wave (N = 8: the 8-value ramp; N = 6, FIXED: the 6-value ramp with 0 and 255);
 // every lane holds v[] and gets the mode's error and block.  row: 16 floats of
-// LDS, the wave's own.  The block kernels run the two modes on two waves at once
-// and join them with bc4_pick.
+// LDS, the wave's own (80 floats: the sorted values, the compacted entries and
+// the cluster step's per-texel results).  The block kernels run the two modes on
+// two waves at once and join them with bc4_pick.
 template <int N, bool FIXED>
 __device__ __forceinline__ float encode_bc4_mode_wave(const float v[16], float *row, uint64_t &block)
 {
     float s[16];
     bc4_sort_wave(v, s, row);
     float ramp[2];
-    scalar_endpoints_wave<N, FIXED>(ramp, s);
+    scalar_endpoints_wave<N, FIXED>(ramp, s, row);
     uint64_t ib;
-    const float e = scalar_cluster<N, FIXED>(v, ramp, ib);
-    const uint8_t e0 = (uint8_t)ramp[0], e1 = (uint8_t)ramp[1];
+    const float e = scalar_cluster_wave<N, FIXED>(v, ramp, ib, row);
+    // the reference's (uint8_t) of a ramp end: a conversion to int and its low
+    // byte (the 8-value mode's one-value ramp 255 / 256 stores 256 as 0); the
+    // bare float-to-uint8_t conversion let the compiler join the fields with an
+    // add, carrying that 256 into the next byte
+    const uint32_t e0 = (uint8_t)(int)ramp[0], e1 = (uint8_t)(int)ramp[1];
     block = (uint64_t)e0 | ((uint64_t)e1 << 8) | (ib << 16);
     return e;
 }
@@ -2274,7 +2342,7 @@ __global__ void __launch_bounds__(192) bc23_blocks_wave_kernel(const float *__re
     __shared__ uint2 res;
     __shared__ uint64_t ares[2];
     __shared__ float aerr[2];
-    __shared__ float ucol[224], arow[2][16];
+    __shared__ float ucol[224], arow[2][80];
     const uint32_t id = blockIdx.x;
     if (id >= n) return;
     float blk[64];
@@ -2320,7 +2388,7 @@ __global__ void __launch_bounds__(192) bc23_blocks_wave_kernel(const float *__re
 __global__ void __launch_bounds__(128) bc4_blocks_wave_kernel(const float *__restrict__ blocks, uint32_t n,
                                                               uint64_t *__restrict__ dst)
 {
-    __shared__ float srow[2][16];
+    __shared__ float srow[2][80];
     __shared__ uint64_t res[2];
     __shared__ float err[2];
     const uint32_t id = blockIdx.x;
