@@ -1210,6 +1210,21 @@ struct TexF {
     __device__ __forceinline__ bool transparent(int i) const { return !(in[i * 4 + 3] * 255.0f >= thr); }
     __device__ __forceinline__ const TexF &view() const { return *this; }
 };
+// One texel per lane for the one-wave kernels' final clustering (lane i < 16
+// holds texel i, read from the block with a vector load, so the wave-uniform
+// copy of the block need not stay live through the endpoint search)
+struct TexW {
+    float c[4];   // R, G, B, A as stored
+    float thr;    // thr01 * 255.f
+    __device__ __forceinline__ TexW(const float *__restrict__ blk, float thr_) : thr(thr_)
+    {
+        const int t = (int)(threadIdx.x & 15u);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c[k] = blk[t * 4 + k];
+    }
+    __device__ __forceinline__ float ch(int k) const { return c[k] * 255.0f; }
+    __device__ __forceinline__ bool transparent() const { return !(c[3] * 255.0f >= thr); }
+};
 // The block's texels by value (TexG::view)
 struct TexV {
     uint32_t px[16];
@@ -1257,17 +1272,17 @@ struct TexL {
     }
 };
 
-// Clstr -> ClstrBas -> ClstrIntnl, amd_bcx_body.cpp:258-378
-template <int N, class Tex>
-__device__ __forceinline__ uint32_t final_indices(const Tex &tex, const uint8_t ep[3][2], bool use_alpha, float &err)
+// Clstr -> ClstrBas -> ClstrIntnl, amd_bcx_body.cpp:258-378: the ramp colours
+// (nr of them: 1 for a flat ramp) ...
+template <int N>
+__device__ __forceinline__ int final_ramp(const uint8_t ep[3][2], float r[3][4])
 {
-    const float w0 = 0.3086f, w1 = 0.6094f, w2 = 0.0820f;
     const unsigned c0 = ((unsigned)(ep[CH_R][0] & 0xf8) << 8) | ((unsigned)(ep[CH_G][0] & 0xfc) << 3) |
                         ((unsigned)(ep[CH_B][0] & 0xf8) >> 3);
     const unsigned c1 = ((unsigned)(ep[CH_R][1] & 0xf8) << 8) | ((unsigned)(ep[CH_G][1] & 0xfc) << 3) |
                         ((unsigned)(ep[CH_B][1] & 0xf8) >> 3);
     const bool swap = (!(N & 1) && c0 <= c1) || ((N & 1) && c0 > c1);
-    float ends[3][2], wk[3][2], r[3][4];
+    float ends[3][2], wk[3][2];
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
         ends[ch][0] = (float)ep[ch][swap ? 1 : 0];
@@ -1276,39 +1291,86 @@ __device__ __forceinline__ uint32_t final_indices(const Tex &tex, const uint8_t 
     const bool flat = expand_grid(wk, ends);
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) chan_ramp<N>(r[ch], wk[ch]);
-    const int nr = flat ? 1 : N;
+    return flat ? 1 : N;
+}
+
+// ... one texel's index (N for a transparent texel) and error term (0 then)
+template <int N>
+__device__ __forceinline__ uint32_t final_texel(float R, float G, float B, bool transparent, const float r[3][4], int nr,
+                                                float &term)
+{
+    const float w0 = 0.3086f, w1 = 0.6094f, w2 = 0.0820f;
+    term = 0.f;
+    if (transparent) return N;
+    float best = 99999999999.f;
+    int bi = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        if (k >= nr) break;
+        const float d = (R - r[CH_R][k]) * (R - r[CH_R][k]) * w0 + (G - r[CH_G][k]) * (G - r[CH_G][k]) * w1 +
+                        (B - r[CH_B][k]) * (B - r[CH_B][k]) * w2;
+        if (d < best) {
+            best = d;
+            bi = k;
+        }
+    }
+    term = best;
+    if (bi == N - 1)
+        bi = 1;
+    else if (bi)
+        bi++;
+    return (uint32_t)bi;
+}
+
+// ... and the block's indices, the error summed in texel order
+template <int N, class Tex>
+__device__ __forceinline__ uint32_t final_indices(const Tex &tex, const uint8_t ep[3][2], bool use_alpha, float &err)
+{
+    float r[3][4];
+    const int nr = final_ramp<N>(ep, r);
     uint32_t bits = 0;
     err = 0.f;
     const auto &t = tex.view();
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        const float R = t.ch(i, 0), G = t.ch(i, 1), B = t.ch(i, 2);
-        uint32_t idx;
-        if (use_alpha && t.transparent(i)) {
-            idx = N;
-        } else {
-            float best = 99999999999.f;
-            int bi = 0;
-#pragma unroll
-            for (int k = 0; k < N; ++k) {
-                if (k >= nr) break;
-                const float d = (R - r[CH_R][k]) * (R - r[CH_R][k]) * w0 + (G - r[CH_G][k]) * (G - r[CH_G][k]) * w1 +
-                                (B - r[CH_B][k]) * (B - r[CH_B][k]) * w2;
-                if (d < best) {
-                    best = d;
-                    bi = k;
-                }
-            }
-            err += best;
-            if (bi == N - 1)
-                bi = 1;
-            else if (bi)
-                bi++;
-            idx = (uint32_t)bi;
-        }
+        float term;
+        const bool tr = use_alpha && t.transparent(i);
+        const uint32_t idx = final_texel<N>(t.ch(i, 0), t.ch(i, 1), t.ch(i, 2), tr, r, nr, term);
+        if (!tr) err += term;
         bits |= (idx & 3u) << (2 * i);
     }
     return bits;
+}
+
+// 16 bits spread to the even bits of a word
+__device__ __forceinline__ uint32_t spread_even(uint32_t x)
+{
+    x = (x | (x << 8)) & 0x00ff00ffu;
+    x = (x | (x << 4)) & 0x0f0f0f0fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    return (x | (x << 1)) & 0x55555555u;
+}
+
+// final_indices for the one-wave kernels: lane i < 16 clusters texel i, the
+// index bits come from two ballots and every lane sums the terms in texel order
+// from an LDS row (16 floats; a transparent texel's +0 leaves the sum as the
+// skipped addition does, the sum being >= +0 or NaN)
+template <int N>
+__device__ __forceinline__ uint32_t final_indices_wave(const TexW &t, const uint8_t ep[3][2], bool use_alpha, float &err,
+                                                       float *row)
+{
+    float r[3][4];
+    const int nr = final_ramp<N>(ep, r);
+    const int L = (int)(threadIdx.x & 63u);
+    float term;
+    const uint32_t idx = final_texel<N>(t.ch(0), t.ch(1), t.ch(2), use_alpha && t.transparent(), r, nr, term);
+    const uint32_t lo = (uint32_t)__ballot(L < 16 && (idx & 1u)), hi = (uint32_t)__ballot(L < 16 && (idx & 2u));
+    if (L < 16) row[L] = term;
+    wave_sync_lds();
+    err = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) err += row[i];
+    return spread_even(lo & 0xffffu) | (spread_even(hi & 0xffffu) << 1);
 }
 
 // CompRGBABlock, amd_bcx_body.cpp:1209-1297.  Returns the float error (FLT_MAX
@@ -1335,7 +1397,10 @@ __device__ __forceinline__ float comp_rgba(const Tex &t, int steps, bool use_alp
         ep[ch][1] = (uint8_t)res[ch][1];
     }
     float err;
-    ibits = final_indices<N>(t, ep, use_alpha, err);
+    if constexpr (WAVE && LaneRows<Col>::v)
+        ibits = final_indices_wave<N>(t, ep, use_alpha, err, u.urow + 128);   // the projection rows, free again
+    else
+        ibits = final_indices<N>(t, ep, use_alpha, err);
     return err;
 }
 
@@ -2310,7 +2375,7 @@ __global__ void __launch_bounds__(128) bc1_blocks_wave_kernel(const float *__res
     bcx::ColFW u;
     int kept;
     bcx::unique_colours_wave(u, blk, use_alpha, thr01, kept, ucol[threadIdx.x >> 6]);
-    const bcx::TexF t{blk, thr01 * 255.f};
+    const bcx::TexW t(blocks + (size_t)id * 64, thr01 * 255.f);
     const int w = (int)(threadIdx.x >> 6);
     uint8_t ep[3][2];
     uint32_t ib = 0;
@@ -2372,7 +2437,7 @@ __global__ void __launch_bounds__(192) bc23_blocks_wave_kernel(const float *__re
         bcx::ColFW u;
         int kept;
         bcx::unique_colours_wave(u, blk, false, 0.f, kept, ucol);
-        const bcx::TexF t{blk, 0.f};
+        const bcx::TexW t(blocks + (size_t)id * 64, 0.f);
         const uint2 r2 = bcx::encode_rgb4<false, true>(u, kept, t, p.steps);
         if (threadIdx.x == 0) res = r2;
     }
