@@ -57,6 +57,7 @@ __constant__ uint8_t dAnchor3b[64];
 constexpr int kQuantTasks = 273;   // m0:16, m1:64, m2:64, m3:64, m6:1, m7:64
 constexpr int kShakeSlots = 6;     // modes 0,1,2,3,6,7
 constexpr int kShakeRanks = 8;
+constexpr uint32_t kSelectWaveBlocks = 4096;   // calls below this select with a wave per block
 constexpr int kDualTasks = 12;     // mode 4: 4 rot x 2 sel, mode 5: 4 rot
 // Distinct (subset mask, cluster count) problems among the subsets of modes
 // 0-3's partitions (k_quant_sub): 150 with 8 clusters, 242 with 4, of 496.
@@ -2421,6 +2422,66 @@ __global__ void __launch_bounds__(256) k_dual(Params p, Workspace ws, const SpEn
 // K4: mode selection in the reference's visiting order (CompressBlock :1400-1447)
 // Mode visit order positions [k0, k1) of CompressBlock's loop; `resume`
 // continues from the state an earlier stage stored, k1 == 8 writes the block.
+// k_select's per-mode steps.  A dual-index mode's candidate t (mode 4: 8
+// rotation x selector tasks, mode 5: 4 rotations) and its score, false when the
+// candidate was not shaken (skipped by the choice)
+__device__ __forceinline__ bool select_dual_score(const Workspace &ws, uint32_t b, int m, int t, double &v)
+{
+    const int t0 = m == 4 ? 0 : 8;
+    const DualResult &dr = ws.dual[(size_t)b * kDualTasks + t0 + t];
+    if (dr.err[0] == 1.7976931348623157e308) return false;   // candidate not shaken
+    v = 0;
+    v += dr.err[0];
+    v += dr.err[1] / 3.;
+    return true;
+}
+
+// a single-index mode's rank r: its subsets' errors summed in subset order
+__device__ __forceinline__ double select_single_score(const Workspace &ws, uint32_t b, int m, int r)
+{
+    const int slot = m <= 3 ? m : (m == 6 ? 4 : 5);
+    const int ns = kModes[m].subsets;
+    const ShakeResult *shk = ws.shk + ((size_t)b * kShakeSlots + slot) * kShakeRanks;
+    double v = 0;
+    for (int s = 0; s < ns; ++s) v += shake_ref(shk, r, s).err[shake_sub(shk, r, s)];
+    return v;
+}
+
+// the block words of mode m's chosen candidate bi
+__device__ __forceinline__ void select_pack(const Workspace &ws, uint32_t b, int m, int bi, uint32_t w[4])
+{
+    if (m == 4 || m == 5) {
+        const int t0 = m == 4 ? 0 : 8;
+        const DualResult &dr = ws.dual[(size_t)b * kDualTasks + t0 + bi];
+        int ep[2][2][4], idx[2][16];
+        for (int h = 0; h < 2; ++h) {
+            for (int q = 0; q < 4; ++q) {
+                ep[h][0][q] = dr.ep[h][0][q];
+                ep[h][1][q] = dr.ep[h][1][q];
+            }
+            for (int q = 0; q < 16; ++q) idx[h][q] = (int)((dr.idx[h] >> (4 * q)) & 15u);
+        }
+        const int task = t0 + bi;
+        const int rot = task < 8 ? (task >> 1) : (task - 8);
+        const int sel = task < 8 ? (task & 1) : 0;
+        pack_dual(m, sel, rot, ep, idx, w);
+    } else {
+        const int slot = m <= 3 ? m : (m == 6 ? 4 : 5);
+        const int ns = kModes[m].subsets;
+        const ShakeResult *shk = ws.shk + ((size_t)b * kShakeSlots + slot) * kShakeRanks;
+        uint8_t ep[3][2][4];
+        uint64_t tidx = 0;
+        for (int s = 0; s < ns; ++s) {   // repeated subsets: their first occurrence
+            const ShakeResult &src = shake_ref(shk, bi, s);
+            const int ss = shake_sub(shk, bi, s);
+            tidx |= src.idx[ss];
+            for (int k = 0; k < 2; ++k)
+                for (int c = 0; c < 4; ++c) ep[s][k][c] = src.ep[ss][k][c];
+        }
+        pack_single(m, (int)shk[bi].part, ep, tidx, w);
+    }
+}
+
 __global__ void __launch_bounds__(256) k_select(Params p, Workspace ws, uint4 *__restrict__ dst, double *__restrict__ err_out,
                                                 int k0, int k1, int resume)
 {
@@ -2452,65 +2513,32 @@ __global__ void __launch_bounds__(256) k_select(Params p, Workspace ws, uint4 *_
         const int m = order[k];
         if (meta.flags & 4u) break;
         if (!((p.probe ? meta.pvalid : meta.valid) & (1u << m))) continue;
-        double e;
-        uint32_t w[4];
+        double be = 1.7976931348623157e308;
+        int bi = 0;
         if (m == 4 || m == 5) {
-            const int t0 = m == 4 ? 0 : 8, nt = m == 4 ? 8 : 4;
-            int bi = 0;
-            double be = 1.7976931348623157e308;
+            const int nt = m == 4 ? 8 : 4;
             for (int t = 0; t < nt; ++t) {
-                const DualResult &dr = ws.dual[(size_t)b * kDualTasks + t0 + t];
-                if (dr.err[0] == 1.7976931348623157e308) continue;   // candidate not shaken
-                double v = 0;
-                v += dr.err[0];
-                v += dr.err[1] / 3.;
+                double v;
+                if (!select_dual_score(ws, b, m, t, v)) continue;
                 if (v < be) {
                     be = v;
                     bi = t;
                 }
             }
-            e = be;
-            const DualResult &dr = ws.dual[(size_t)b * kDualTasks + t0 + bi];
-            int ep[2][2][4], idx[2][16];
-            for (int h = 0; h < 2; ++h) {
-                for (int q = 0; q < 4; ++q) {
-                    ep[h][0][q] = dr.ep[h][0][q];
-                    ep[h][1][q] = dr.ep[h][1][q];
-                }
-                for (int q = 0; q < 16; ++q) idx[h][q] = (int)((dr.idx[h] >> (4 * q)) & 15u);
-            }
-            const int task = t0 + bi;
-            const int rot = task < 8 ? (task >> 1) : (task - 8);
-            const int sel = task < 8 ? (task & 1) : 0;
-            pack_dual(m, sel, rot, ep, idx, w);
         } else {
-            const int slot = m <= 3 ? m : (m == 6 ? 4 : 5);
             const int attempts = mode_attempts(p, m);
-            const int ns = kModes[m].subsets;
-            int bi = 0;
-            double be = 1.7976931348623157e308;
-            const ShakeResult *shk = ws.shk + ((size_t)b * kShakeSlots + slot) * kShakeRanks;
             for (int r = 0; r < attempts; ++r) {
-                double v = 0;
-                for (int s = 0; s < ns; ++s) v += shake_ref(shk, r, s).err[shake_sub(shk, r, s)];
+                const double v = select_single_score(ws, b, m, r);
                 if (v < be) {
                     be = v;
                     bi = r;
                 }
                 if (p.err_thr > 0 && be <= p.err_thr) break;   // :837-843
             }
-            e = be;
-            uint8_t ep[3][2][4];
-            uint64_t tidx = 0;
-            for (int s = 0; s < ns; ++s) {   // repeated subsets: their first occurrence
-                const ShakeResult &src = shake_ref(shk, bi, s);
-                const int ss = shake_sub(shk, bi, s);
-                tidx |= src.idx[ss];
-                for (int k = 0; k < 2; ++k)
-                    for (int c = 0; c < 4; ++c) ep[s][k][c] = src.ep[ss][k][c];
-            }
-            pack_single(m, (int)shk[bi].part, ep, tidx, w);
         }
+        const double e = be;
+        uint32_t w[4];
+        select_pack(ws, b, m, bi, w);
         if (p.decode_select) {
             const double d = decoded_sse(w, tex);
             if (d < best_d) {
@@ -2527,6 +2555,106 @@ __global__ void __launch_bounds__(256) k_select(Params p, Workspace ws, uint4 *_
             break;
         }
     }
+    if (k1 < 8) {
+        ws.best_err[b] = best;
+        ws.best_blk[b] = make_uint4(bw[0], bw[1], bw[2], bw[3]);
+        ws.meta[b].flags = meta.flags;
+        return;
+    }
+    dst[out_id] = make_uint4(bw[0], bw[1], bw[2], bw[3]);
+    if (err_out) err_out[out_id] = best;
+}
+
+// k_select for small calls (the block-level entry points): one wave per block.
+// Lane 8 k + c scores candidate c of the k-th mode in selection order -- the
+// serial kernel's dependent global loads, ~85 us for one block, issued at once --
+// and lane 0 replays k_select's choice over the scores from LDS (the same
+// comparisons in the same order), then packs only the chosen mode's block.
+// Not for the decode-aware choice (bounded-exit probes), which packs every mode.
+__global__ void __launch_bounds__(64) k_select_wave(Params p, Workspace ws, uint4 *__restrict__ dst,
+                                                    double *__restrict__ err_out, int k0, int k1, int resume)
+{
+    __shared__ double score[64];
+    const uint32_t b = blockIdx.x;
+    if (b >= p.n) return;
+    const int L = (int)threadIdx.x;
+    BlockMeta meta = ws.meta[b];
+    const uint32_t out_id = out_block(p, b);
+    if (meta.flags & 1u) {
+        if (k1 == 8 && L == 0) {
+            dst[out_id] = make_uint4(0, 0, 0, 0);
+            if (err_out) err_out[out_id] = -1.0;
+        }
+        return;
+    }
+    if (p.skip_done && (meta.flags & 4u)) return;   // written by k_bound
+    const int order[8] = {6, 4, 3, 1, 2, 0, 7, 5};
+    bool has = false;
+    {
+        const int k = L >> 3, c = L & 7, m = order[k];
+        double v = 0;
+        if (k >= k0 && k < k1 && ((p.probe ? meta.pvalid : meta.valid) & (1u << m))) {
+            if (m == 4 || m == 5)
+                has = c < (m == 4 ? 8 : 4) && select_dual_score(ws, b, m, c, v);
+            else if (c < mode_attempts(p, m)) {
+                v = select_single_score(ws, b, m, c);
+                has = true;
+            }
+        }
+        score[L] = v;
+    }
+    const uint64_t present = __ballot(has);
+    __syncthreads();
+    if (L != 0) return;
+    double best = 1.7976931348623157e308;
+    uint32_t bw[4] = {0, 0, 0, 0};
+    if (resume) {
+        best = ws.best_err[b];
+        const uint4 v = ws.best_blk[b];
+        bw[0] = v.x;
+        bw[1] = v.y;
+        bw[2] = v.z;
+        bw[3] = v.w;
+    }
+    int win_m = -1, win_bi = 0;
+    for (int k = k0; k < k1; ++k) {
+        const int m = order[k];
+        if (meta.flags & 4u) break;
+        if (!((p.probe ? meta.pvalid : meta.valid) & (1u << m))) continue;
+        double be = 1.7976931348623157e308;
+        int bi = 0;
+        if (m == 4 || m == 5) {
+            const int nt = m == 4 ? 8 : 4;
+            for (int t = 0; t < nt; ++t) {
+                if (!((present >> (8 * k + t)) & 1u)) continue;   // not shaken
+                const double v = score[8 * k + t];
+                if (v < be) {
+                    be = v;
+                    bi = t;
+                }
+            }
+        } else {
+            const int attempts = mode_attempts(p, m);
+            for (int r = 0; r < attempts; ++r) {
+                const double v = score[8 * k + r];
+                if (v < be) {
+                    be = v;
+                    bi = r;
+                }
+                if (p.err_thr > 0 && be <= p.err_thr) break;   // :837-843
+            }
+        }
+        if (be < best) {
+            best = be;
+            win_m = m;
+            win_bi = bi;
+        }
+        if (p.err_thr > 0 && best <= p.err_thr) {   // CompressBlock :1440-1446
+            meta.flags |= 4u;
+            break;
+        }
+    }
+    if (win_m >= 0) select_pack(ws, b, win_m, win_bi, bw);
     if (k1 < 8) {
         ws.best_err[b] = best;
         ws.best_blk[b] = make_uint4(bw[0], bw[1], bw[2], bw[3]);
@@ -3249,8 +3377,12 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
                 const hipError_t re = run_modes(p, ws, st->sp, s, integral);
                 if (re != hipSuccess) return re;
             }
-            hipLaunchKernelGGL(k_select, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, p, ws, (uint4 *)dst, err,
-                               staged ? k : 0, staged ? k + 1 : 8, resume);
+            if (p.n < kSelectWaveBlocks && !p.decode_select)
+                hipLaunchKernelGGL(k_select_wave, dim3(p.n), dim3(64), 0, s, p, ws, (uint4 *)dst, err, staged ? k : 0,
+                                   staged ? k + 1 : 8, resume);
+            else
+                hipLaunchKernelGGL(k_select, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, p, ws, (uint4 *)dst, err,
+                                   staged ? k : 0, staged ? k + 1 : 8, resume);
             resume = 1;
         }
         return hipGetLastError();
