@@ -485,6 +485,35 @@ __device__ __forceinline__ void refine_pass3(float cur[3][2], const float base[3
     cur[CH][1] = b1;
 }
 
+// ramp_fit_error for the one-wave kernels: lane i < n forms colour i's term from
+// the wave's LDS colour rows, every lane sums the 16 terms in colour order from
+// `row` (colours past n: +0, as the count-0 entries add)
+template <int N>
+__device__ __forceinline__ float ramp_fit_error_wave(const ColFW &u, const float r[3][4], bool flat, float *row)
+{
+    const float w0 = 0.3086f, w1 = 0.6094f, w2 = 0.0820f;
+    const int nr = flat ? 1 : N;
+    const int L = (int)(threadIdx.x & 63u);
+    float term = 0.f;
+    if (L < u.n) {
+        const float cr = u.urow[L * 8 + CH_R], cg = u.urow[L * 8 + CH_G], cb = u.urow[L * 8 + CH_B];
+        float best = 99999999999.f;
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            float d = (cr - r[CH_R][k]) * (cr - r[CH_R][k]) * w0 + (cg - r[CH_G][k]) * (cg - r[CH_G][k]) * w1 +
+                      (cb - r[CH_B][k]) * (cb - r[CH_B][k]) * w2;
+            best = (k < nr && d < best) ? d : best;
+        }
+        term = best * u.urow[L * 8 + 3];
+    }
+    if (L < 16) row[L] = term;
+    wave_sync_lds();
+    float err = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) err += row[i];
+    return err;
+}
+
 template <int N, bool WAVE = false, class Col>
 __device__ __forceinline__ void refine_channels(float cur[3][2], const Col &u, int steps)
 {
@@ -497,7 +526,11 @@ __device__ __forceinline__ void refine_channels(float cur[3][2], const Col &u, i
     const bool flat = expand_grid(wk, cur);
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) chan_ramp<N>(r[ch], wk[ch]);
-    float best = ramp_fit_error<N>(regs(u), r, flat);
+    float best;
+    if constexpr (WAVE && LaneRows<Col>::v)
+        best = ramp_fit_error_wave<N>(u, r, flat, u.urow + 128);   // the projection rows, free again
+    else
+        best = ramp_fit_error<N>(regs(u), r, flat);
     if (best == 0.f || !steps) return;
     const int lo = -(int)minr((float)steps, 8.f), hi = (int)minr((float)steps, 8.f);
     if constexpr (Col::kRefine3) {   // steps == 1 (the kernel's precondition)
