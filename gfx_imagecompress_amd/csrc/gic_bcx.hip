@@ -343,6 +343,61 @@ __device__ __forceinline__ void refine_pass(float cur[3][2], const float base[3]
         const int span = hi - lo + 1, ln = (int)(threadIdx.x & 63u);
         float be = __builtin_huge_valf();
         int bo = 0x7fffffff;
+        if constexpr (LaneRows<Col>::v) {
+            if (span == 3) {
+                // steps == 1: the 9 candidates x 16 colours on the lanes, each
+                // (candidate, colour) term into an LDS row, then candidate t's
+                // lane sums its 16 terms in colour order (the same additions)
+                float *tm = u.urow + 224;
+                const float *y = u.urow + 160;
+                for (int q = ln; q < 144; q += 64) {
+                    const int t = q >> 4, i = q & 15;
+                    float c2[3][2], w2[3][2], rr[4];
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        c2[c][0] = cur[c][0];
+                        c2[c][1] = cur[c][1];
+                    }
+                    c2[CH][0] = minr(maxr(base[CH][0] + (float)(lo + t / 3) * grid, 0.f), 255.f);
+                    c2[CH][1] = minr(maxr(base[CH][1] + (float)(lo + t % 3) * grid, 0.f), 255.f);
+                    const bool flat = expand_grid(w2, c2);
+                    chan_ramp<N>(rr, w2[CH]);
+                    const int nr = flat ? 1 : N;
+                    float term = 0.f;
+                    if (i < u.n) {
+                        const float ci = u.urow[i * 8 + CH];
+                        float m = 10000000.f;
+#pragma unroll
+                        for (int k = 0; k < N; ++k) {
+                            float d = rr[k] - ci;
+                            float e = y[i * 4 + k] + d * d * wc;
+                            m = (k < nr) ? minr(m, e) : m;
+                        }
+                        term = m * u.urow[i * 8 + 3];
+                    }
+                    tm[q] = term;
+                }
+                wave_sync_lds();
+                if (ln < 9) {
+                    float mse = 0.f;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) mse += tm[ln * 16 + i];
+                    if (mse < best) {
+                        be = mse;
+                        bo = ln;
+                    }
+                }
+                wave_argmin(be, bo);
+                if (bo != 0x7fffffff) {
+                    b0 = minr(maxr(base[CH][0] + (float)(lo + bo / span) * grid, 0.f), 255.f);
+                    b1 = minr(maxr(base[CH][1] + (float)(lo + bo % span) * grid, 0.f), 255.f);
+                    best = be;
+                }
+                cur[CH][0] = b0;
+                cur[CH][1] = b1;
+                return;
+            }
+        }
         for (int t = ln; t < span * span; t += 64) {
             const int a = lo + t / span, b = lo + t % span;
             cur[CH][0] = minr(maxr(base[CH][0] + (float)a * grid, 0.f), 255.f);
@@ -1148,8 +1203,9 @@ __device__ __forceinline__ void unique_colours(ColF &u, const float in[64], bool
 // unique_colours for the one-wave block kernels: every lane holds the block (its
 // 64 floats are wave-uniform), lane i < 16 ranks texel i against the others
 // (16 comparisons instead of every lane running all 256), each leader stores
-// its colour at its unique index in the wave's LDS rows (224 floats), and every lane
-// reads the row back.  The keys, counts and ranks are the ones unique_colours
+// its colour at its unique index in the wave's LDS rows (368 floats: colours
+// 0..127, projections 128..159, products and side terms 160..223, Refine terms
+// 224..367), and every lane reads the row back.  The keys, counts and ranks are the ones unique_colours
 // computes, so ColF is identical.  (All lanes running the 16 x 16 comparisons on
 // wave-uniform values took half of a BC1 block call: ~87 K cycles.)
 __device__ __forceinline__ void unique_colours_wave(ColFW &u, const float in[64], bool use_alpha, float thr01, int &kept,
@@ -2397,7 +2453,7 @@ __global__ void __launch_bounds__(128) bc1_blocks_wave_kernel(const float *__res
 {
     __shared__ uint2 res[2];
     __shared__ float err[2];
-    __shared__ float ucol[2][224];
+    __shared__ float ucol[2][368];
     const uint32_t id = blockIdx.x;
     if (id >= n) return;
     float blk[64];
@@ -2440,7 +2496,7 @@ __global__ void __launch_bounds__(192) bc23_blocks_wave_kernel(const float *__re
     __shared__ uint2 res;
     __shared__ uint64_t ares[2];
     __shared__ float aerr[2];
-    __shared__ float ucol[224], arow[2][80];
+    __shared__ float ucol[368], arow[2][80];
     const uint32_t id = blockIdx.x;
     if (id >= n) return;
     float blk[64];
