@@ -82,6 +82,9 @@ def parse():
                    help="BC7 bounded-exit legs: per-block MSE under which the probe's block is final (0 = no legs); "
                         "the batch64 workload uses this value too (0 = no exit)")
     p.add_argument("--no-bc7enc", action="store_true", help="skip the bc7enc16 (fast BC7 path) legs")
+    p.add_argument("--no-g2", action="store_true", help="skip the bounded-exit leg on the G2 texture")
+    p.add_argument("--no-host-api", action="store_true",
+                   help="skip the host-image (Image_Compress*) end-to-end leg (N = 1 only)")
     p.add_argument("--bc6h-size", type=int, default=1024,
                    help="BC6H leg: HDR float32 texture width = height (0 = skip the leg)")
     p.add_argument("--bc7-shake-ranks", type=int, default=None,
@@ -461,7 +464,7 @@ def bc7_cpu_sample(args, host, size, by, budget_s):
     return rows, cpu
 
 
-def bc7_leg(args, gic, src, size, split, dev, rank, shake_ranks=0, bound=0.0, ref=None):
+def bc7_leg(args, gic, src, size, split, dev, rank, shake_ranks=0, bound=0.0, ref=None, leg_name=None):
     """configs[3]: BC7 default quality (BC7BlockEncoder quality 1) on the 8K
     texture, one timed pass over the rank's block rows followed by the gather;
     the exact search (`ref` None) also times the CPU restatement on rows spread
@@ -481,14 +484,18 @@ def bc7_leg(args, gic, src, size, split, dev, rank, shake_ranks=0, bound=0.0, re
         gic.encode_device(7, src, size, size, 1, 4, g.local, opts, split.first, split.rows, stream=stream)
     gic.iter_cap_hits(reset=True)
     wall, kern_ms = _timed(split.world, dev, stream, enc, 1, tail=g.tail())
+    stages = gic.last_bc7_stages()
     hits = gic.iter_cap_hits(reset=True)
     res = _rates(split, size, split.by * 4, 1, wall, kern_ms, nd=4)
+    if bound > 0 and len(stages) > 1:
+        res["stage_blocks"] = stages
+        res["probe_exit_share"] = round(1.0 - stages[-1] / max(stages[0], 1), 4)
     res["ms_per_pass"] = res.pop("ms_per_step")
     res["iter_cap_hits"] = hits
     blocks = split.rows * bx
     res["roofline"] = _hbm_roofline(80, blocks, kern_ms)
-    leg = "bc7" if not shake_ranks and not bound else \
-        ("bc7_pruned" if not bound else ("bc7_bounded" if not shake_ranks else "bc7_bounded_pruned"))
+    leg = leg_name or ("bc7" if not shake_ranks and not bound else
+                       ("bc7_pruned" if not bound else ("bc7_bounded" if not shake_ranks else "bc7_bounded_pruned")))
     valu = _valu_roofline(f"valu_{leg}_pass.json", size, by, kern_ms, launch_key="valu_insts_per_pass",
                           scale=split.rows / by)
     if valu is not None:
@@ -525,6 +532,28 @@ def bc7_leg(args, gic, src, size, split, dev, rank, shake_ranks=0, bound=0.0, re
                                  f"MSE contract, mean MSE {mg_sum / n:.4f} vs {mc_sum / n:.4f}" +
                                  (f", {hit} within the exit bound" if bound > 0 else ""))
     return res
+
+
+def g2_bounded_leg(args, gic, size, split, dev, rank):
+    """The bounded exit on a second content: G2 (the same gradient, independent
+    noise per channel, synth.g2) instead of G1's grey-axis noise.  Reports the
+    share of blocks the probes finish (stage_blocks: blocks entering each stage)
+    and checks two exact-oracle rows under the contract."""
+    from gfx_imagecompress_amd import synth
+    src2 = synth.g2_torch(size, size, device=dev)
+    ref = None
+    if rank == 0 and not args.no_cpu:
+        host2 = src2[0].cpu().numpy()
+        orc = _oracle()
+        by = args.bc7_rows if args.bc7_rows > 0 else (size + 3) // 4
+        ref = {r: orc.encode_image_bc7(host2, quality=args.bc7_quality, first_row=r, num_rows=1,
+                                       threads=_cpu_threads()) for r in (0, by // 2)}
+    res = bc7_leg(args, gic, src2, size, split, dev, rank, 0, args.bc7_mse_bound, ref=ref,
+                  leg_name="bc7_bounded_g2")
+    out = dict(metric=f"BC7 q{args.bc7_quality:g}, bounded exit (MSE {args.bc7_mse_bound:g}) + exact survivors, "
+                      f"G2 (independent per-channel noise)", **res)
+    del src2
+    return out
 
 
 def _stream(dev):
@@ -837,6 +866,88 @@ def batch_workload(args, gic, world, rank, dev):
 
 
 # ---------------------------------------------------------------------------
+# the drop-in host path: host image in, host blocks out (Image_Compress*)
+# ---------------------------------------------------------------------------
+
+def host_api_leg(args, gic, src, size, dev, kernel_ms):
+    """Image_CompressAMDBC1 (the reference's entry, NULL options) and the BC7
+    bounded exit (gic_compress_image) on the 8K host image, end to end: the
+    upload of the pageable source, the pipelined encode and the download into
+    the returned header.  Beside it the same bytes moved alone (a pageable and a
+    pinned 256 MiB upload) and the device-resident kernel time, so the line shows
+    how close the pipeline gets to max(upload, kernel)."""
+    import numpy as np
+    import torch
+    host = np.ascontiguousarray(src[0].cpu().numpy())
+    mpix = size * size / 1e6
+
+    def timed_copy(t_src, reps=3):
+        d = torch.empty(t_src.shape, dtype=t_src.dtype, device=dev)
+        best = 1e30
+        for _ in range(reps):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            d.copy_(t_src)
+            torch.cuda.synchronize(dev)
+            best = min(best, time.perf_counter() - t0)
+        return best * 1e3
+
+    pageable_ms = timed_copy(torch.from_numpy(host))
+    pinned_ms = timed_copy(torch.from_numpy(host).pin_memory())
+    want1 = torch.empty((size // 4) * (size // 4) * 8, dtype=torch.uint8, device=dev)
+    gic.encode_device(1, src, size, size, 1, 4, want1, gic.Options())
+    want1 = want1.cpu().numpy()
+    out = {"note": "end to end = host header in -> pipelined upload / encode / download -> host header out; "
+                   "pieces of 2^18 blocks (BC7 2^20); GIC_H2D selects the upload mode",
+           "upload_alone_ms": {"pageable": round(pageable_ms, 3), "pinned": round(pinned_ms, 3)},
+           "bc1_kernel_ms": round(kernel_ms, 4)}
+    modes = {}
+    old = os.environ.get("GIC_H2D")
+    hi = gic.HostImage(host)
+    try:
+        for mode in ("pageable", "staged", "register"):
+            os.environ["GIC_H2D"] = mode
+            times, rep_best, ok = [], None, True
+            for _ in range(1 + 3):
+                got = hi.compress(1, entry="Image_CompressAMDBC1")
+                ok = ok and got is not None and np.array_equal(got.reshape(-1), want1)
+                rep = gic.host_report()
+                times.append(hi.last_call_ms)
+                if rep_best is None or rep["total_ms"] < rep_best["total_ms"]:
+                    rep_best = rep
+            e2e = min(times[1:])
+            bound = max(pageable_ms if mode == "pageable" else pinned_ms, kernel_ms)
+            modes[mode] = {"e2e_ms": round(e2e, 3), "mpix_s": round(mpix / (e2e / 1e3), 1),
+                           "h2d_ms": round(rep_best["h2d_ms"], 3), "encode_ms": round(rep_best["encode_ms"], 3),
+                           "d2h_ms": round(rep_best["d2h_ms"], 3), "pieces": rep_best["pieces"],
+                           "e2e_over_max_upload_kernel": round(e2e / bound, 3),
+                           "bytes_equal_device_path": bool(ok)}
+        best = min(modes, key=lambda m: modes[m]["e2e_ms"])
+        out["bc1"] = dict(mode=best, **modes[best])
+        out["bc1_modes"] = modes
+        os.environ["GIC_H2D"] = best
+        if args.bc7_rows != 0:
+            o = gic.Options(bc7_mse_bound=0.5)
+            times = []
+            for _ in range(2):
+                got7 = hi.compress(7, o)
+                times.append(hi.last_call_ms)
+            rep = gic.host_report()
+            out["bc7_bounded"] = {"mode": best, "e2e_ms": round(min(times), 2),
+                                  "mpix_s": round(mpix / (min(times) / 1e3), 1),
+                                  "h2d_ms": round(rep["h2d_ms"], 3), "encode_ms": round(rep["encode_ms"], 2),
+                                  "d2h_ms": round(rep["d2h_ms"], 3), "pieces": rep["pieces"],
+                                  "blocks": int(got7.size // 16)}
+    finally:
+        hi.close()
+        if old is None:
+            os.environ.pop("GIC_H2D", None)
+        else:
+            os.environ["GIC_H2D"] = old
+    return out
+
+
+# ---------------------------------------------------------------------------
 # the 8K workload (configs[1]-[3]) and the headline line
 # ---------------------------------------------------------------------------
 
@@ -913,6 +1024,8 @@ def main():
     del g
 
     legs = {}
+    if fmt == 1 and world == 1 and not args.no_host_api:
+        legs["host_api"] = host_api_leg(args, gic, src, size, dev, head["kernel_ms"])
     if fmt == 1 and not args.no_bc45:
         for f in (4, 5):
             legs[f"bc{f}"] = bc45_leg(args, gic, f, Split(by, world, rank, args.weak), dev, rank)
@@ -957,6 +1070,8 @@ def main():
             bc7["bc7_bounded"] = dict(
                 metric=f"BC7 q{q:g}, bounded exit (MSE {args.bc7_mse_bound:g}) + exact survivors",
                 **bc7_leg(args, gic, src, size, split, dev, rank, 0, args.bc7_mse_bound, ref=ref))
+            if not args.no_g2:
+                bc7["bc7_bounded_g2"] = g2_bounded_leg(args, gic, size, split, dev, rank)
         bc7["bc7"] = exact
     elif fmt == 7 and rank == 0:
         roof["valu_dominant"] = _dominant_kernel("valu_bc7_shake8.json")

@@ -132,6 +132,20 @@ class _MultiReport(ctypes.Structure):
                 ("gather_ms", ctypes.c_double), ("gathered_bytes", ctypes.c_uint64)]
 
 
+class _HostReport(ctypes.Structure):
+    _fields_ = [("devices", ctypes.c_int), ("pieces", ctypes.c_int), ("h2d_mode", ctypes.c_int),
+                ("total_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double), ("encode_ms", ctypes.c_double),
+                ("d2h_ms", ctypes.c_double)]
+
+
+class _ImageHeader(ctypes.Structure):   # include/gfx_image/image.h
+    _fields_ = [("dataSize", ctypes.c_uint64), ("width", ctypes.c_uint32), ("height", ctypes.c_uint32),
+                ("depth", ctypes.c_uint32), ("slices", ctypes.c_uint32), ("format", ctypes.c_int),
+                ("flags", ctypes.c_uint32), ("data", ctypes.c_void_p)]
+
+
+PROGRESS_FUNC = ctypes.CFUNCTYPE(ctypes.c_bool, ctypes.c_void_p, ctypes.c_float)
+
 _lib = None
 
 
@@ -190,6 +204,27 @@ def library() -> ctypes.CDLL:
     lib.gic_multi_split.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
                                     ctypes.POINTER(ctypes.c_uint64)]
     lib.gic_multi_split.restype = ctypes.c_int
+    lib.gic_last_bc7_stages.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int)]
+    lib.gic_last_bc7_stages.restype = ctypes.c_int
+    lib.gic_last_host_report.argtypes = [ctypes.POINTER(_HostReport)]
+    lib.gic_last_host_report.restype = ctypes.c_int
+    lib.gic_compress_image.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(_COptions), ctypes.c_void_p,
+                                       ctypes.c_void_p]
+    lib.gic_compress_image.restype = ctypes.c_void_p
+    lib.Image_CreateNoClear.argtypes = [ctypes.c_uint32] * 4 + [ctypes.c_int]
+    lib.Image_CreateNoClear.restype = ctypes.c_void_p
+    lib.Image_Destroy.argtypes = [ctypes.c_void_p]
+    lib.Image_Destroy.restype = None
+    for name in ("Image_CompressAMDBC1",):
+        getattr(lib, name).argtypes = [ctypes.c_void_p] * 5
+        getattr(lib, name).restype = ctypes.c_void_p
+    for name in ("Image_CompressAMDBC2", "Image_CompressAMDBC3", "Image_CompressAMDBC7", "Image_CompressAMDBC6H",
+                 "Image_CompressRichGel999BC7"):
+        getattr(lib, name).argtypes = [ctypes.c_void_p] * 4
+        getattr(lib, name).restype = ctypes.c_void_p
+    for name in ("Image_CompressAMDBC4", "Image_CompressAMDBC5"):
+        getattr(lib, name).argtypes = [ctypes.c_void_p] * 3
+        getattr(lib, name).restype = ctypes.c_void_p
     _lib = lib
     return lib
 
@@ -247,8 +282,13 @@ def encode_multi(fmt: int, image, devices, dst, options: Options | None = None, 
         a = a[None]
     s, h, w, c = a.shape
     bx, by = blocks_shape(w, h)
+    want = {SRC_UNORM8: np.uint8, SRC_SNORM8: np.int8, SRC_FLOAT32: np.float32}.get(src_type)
+    if want is None or a.dtype != want:
+        raise GicError(f"source type {src_type} needs a {want} image, got {a.dtype}")
     if not dst.is_cuda or dst.numel() * dst.element_size() < bx * by * s * block_bytes(fmt):
         raise GicError("dst must be a device tensor holding the whole image's blocks")
+    if not devices or dst.device.index != devices[0]:
+        raise GicError(f"dst must live on devices[0] ({devices[0] if devices else None}), not {dst.device}")
     devs = (ctypes.c_int * len(devices))(*devices)
     opts = (options or Options()).to_c()
     rc = library().gic_encode_multi(fmt, src_type, a.ctypes.data, w, h, s, c, w * c * a.itemsize, ctypes.byref(opts),
@@ -258,6 +298,104 @@ def encode_multi(fmt: int, image, devices, dst, options: Options | None = None, 
     _check(library().gic_multi_last_report(ctypes.byref(r)))
     return {"ranks": r.ranks, "rccl": bool(r.rccl), "encode_ms_max": r.encode_ms_max, "gather_ms": r.gather_ms,
             "gathered_bytes": int(r.gathered_bytes)}
+
+
+# TinyImageFormat of a host source (include/gfx_image/image.h)
+_HOST_FORMATS = {("u1", 1): 1, ("i1", 1): 2, ("u1", 2): 3, ("i1", 2): 4, ("u1", 3): 5, ("u1", 4): 7,
+                 ("f4", 4): 9}
+
+
+def _host_header(lib, a):
+    """An Image_ImageHeader (library-allocated) holding the (S,H,W,C) array a."""
+    s, h, w, c = a.shape
+    key = (a.dtype.kind + str(a.dtype.itemsize), c)
+    if key not in _HOST_FORMATS:
+        raise GicError(f"no host image format for {a.dtype} with {c} channels")
+    p = lib.Image_CreateNoClear(w, h, 1, s, _HOST_FORMATS[key])
+    if not p:
+        raise GicError("Image_CreateNoClear failed")
+    ctypes.memmove(_ImageHeader.from_address(p).data, a.ctypes.data, a.nbytes)
+    return p
+
+
+def last_bc7_stages() -> list[int]:
+    """Blocks entering each stage of this thread's last BC7 call
+    (gic_last_bc7_stages): [all, after the mode-6 probe, after mode 3, after
+    mode 1] with the bounded exit, [all] without."""
+    arr, n = (ctypes.c_uint32 * 4)(), ctypes.c_int(0)
+    _check(library().gic_last_bc7_stages(arr, ctypes.byref(n)))
+    return [int(arr[k]) for k in range(n.value)]
+
+
+def host_report() -> dict:
+    """gic_last_host_report: this thread's last host-image call (devices,
+    pieces, h2d_mode, total_ms and the upload / encode / download spans)."""
+    r = _HostReport()
+    _check(library().gic_last_host_report(ctypes.byref(r)))
+    return {k: getattr(r, k) for k, _ in _HostReport._fields_}
+
+
+class HostImage:
+    """A host image (Image_ImageHeader allocated by the library) holding a numpy
+    array (H,W,C) or (S,H,W,C), uint8 / int8 / float32 (C = 4 for float), for
+    repeated host-path calls.  ``last_call_ms`` is the C call alone (host clock)."""
+
+    def __init__(self, image):
+        import numpy as np
+        a = np.ascontiguousarray(image)
+        if a.ndim == 2:
+            a = a[:, :, None]
+        if a.ndim == 3:
+            a = a[None]
+        self.shape = a.shape
+        self.ptr = _host_header(library(), a)
+        self.last_call_ms = 0.0
+
+    def compress(self, fmt: int, options: Options | None = None, progress=None, entry: str | None = None):
+        """``gic_compress_image`` with explicit options, or with ``entry`` one of
+        the reference's own wrappers (e.g. ``"Image_CompressAMDBC1"``, NULL
+        options).  ``progress``: None or callable(pct) -> bool (True aborts).
+        Returns (S,by,bx,bytes) uint8 blocks, or None when aborted."""
+        import time
+        import numpy as np
+        lib = library()
+        s, h, w, _ = self.shape
+        bx, by = blocks_shape(w, h)
+        cb = PROGRESS_FUNC(lambda user, pct: bool(progress(pct))) if progress else None
+        cbp = ctypes.cast(cb, ctypes.c_void_p) if cb else None
+        opts = (options or Options()).to_c()
+        t0 = time.perf_counter()
+        if entry is None:
+            out = lib.gic_compress_image(self.ptr, fmt, ctypes.byref(opts), cbp, None)
+        else:
+            fn = getattr(lib, entry)
+            extra = {5: [None, None], 4: [None], 3: []}[len(fn.argtypes)]
+            out = fn(self.ptr, *extra, cbp, None)
+        self.last_call_ms = (time.perf_counter() - t0) * 1e3
+        if not out:
+            return None
+        hd = _ImageHeader.from_address(out)
+        blocks = np.ctypeslib.as_array((ctypes.c_uint8 * hd.dataSize).from_address(hd.data)).copy()
+        lib.Image_Destroy(out)
+        return blocks.reshape(s, by, bx, -1)
+
+    def close(self):
+        if self.ptr:
+            library().Image_Destroy(self.ptr)
+            self.ptr = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def compress_host(fmt: int, image, options: Options | None = None, progress=None, entry: str | None = None):
+    """The host-image path (host image in, host blocks out) through the C ABI,
+    one call: see :class:`HostImage`.  The call's timing is :func:`host_report`."""
+    with HostImage(image) as hi:
+        return hi.compress(fmt, options, progress, entry)
 
 
 def multi_split(rows_total: int, ndev: int, i: int) -> tuple[int, int]:

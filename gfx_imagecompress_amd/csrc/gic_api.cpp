@@ -22,6 +22,7 @@
 #include "../../include/gfx_imagecompress/imagecompress.h"
 #include "../../include/gfx_imagecompress_amd/gic.h"
 #include "gic_common.h"
+#include "gic_pipeline.h"
 
 namespace gic {
 hipError_t launch_bc1_image(const Geometry &g, float thr, int steps, int force_alpha_one, int r3d, void *dst,
@@ -55,6 +56,7 @@ hipError_t bc6h_iter_cap(int cap, unsigned long long *hits, int reset);
 hipError_t bc7_nonterm(unsigned long long *n, int reset);
 hipError_t bc6h_nonterm(unsigned long long *n, int reset);
 void bc7_last_h4(uint32_t *rerun, uint32_t *nonterm);
+void bc7_last_stages(uint32_t in[4], int *n);
 }  // namespace gic
 
 static bool is_bc6h(gic_format f) { return f == GIC_FMT_BC6H || f == GIC_FMT_BC6H_SF; }
@@ -71,6 +73,13 @@ static int hip_fail(hipError_t e)
 }
 
 extern "C" int gic_last_hip_error(void) { return t_last_hip_error; }
+
+extern "C" int gic_last_bc7_stages(uint32_t blocks_in[4], int *stages)
+{
+    if (!blocks_in || !stages) return GIC_EINVAL;
+    gic::bc7_last_stages(blocks_in, stages);
+    return GIC_OK;
+}
 
 extern "C" int gic_iter_cap_hits(unsigned long long *hits, int reset)
 {
@@ -529,7 +538,7 @@ extern "C" void *Image_RawDataPtr(Image_ImageHeader const *img) { return img ? i
 extern "C" void Image_CompressInit(void) {}
 extern "C" void Image_CompressDeinit(void) {}
 
-// Device scratch reused by the synchronous host entry points of one thread.
+// Device scratch reused by the synchronous block-level and decode entry points of one thread.
 struct DeviceScratch {
     void *src = nullptr, *dst = nullptr;
     size_t src_bytes = 0, dst_bytes = 0;
@@ -562,32 +571,57 @@ struct DeviceScratch {
 };
 static thread_local DeviceScratch t_scratch;
 
-// GIC_DEVICES: a comma-separated device list for the image-level entry points
+// The calling thread's lane (streams, events, device buffers) for host-image
+// calls on one device; reused across calls, freed at thread exit.
+struct ThreadLane {
+    gic::LaneBuffers lb;
+    ~ThreadLane() { lb.release(); }
+};
+static thread_local ThreadLane t_lane;
+static thread_local gic_host_report t_host_report;
+
+// GIC_DEVICES: a comma-separated device list for the image-level entry points.
+// A list that cannot be parsed in full, or that names a device this process
+// cannot see, is reported once and ignored (the call runs on one device).
 static std::vector<int> env_devices()
 {
     std::vector<int> out;
     const char *e = getenv("GIC_DEVICES");
-    if (!e) return out;
+    if (!e || !*e) return out;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess) return {};
-    for (const char *p = e; *p;) {
+    bool bad = false;
+    for (const char *p = e; *p && !bad;) {
         char *end = nullptr;
         const long v = strtol(p, &end, 10);
-        if (end == p) break;
-        if (v < 0 || v >= count) return {};
+        if (end == p || v < 0 || v >= count || (*end && *end != ',')) {
+            bad = true;
+            break;
+        }
         out.push_back((int)v);
         p = *end == ',' ? end + 1 : end;
-        if (*end && *end != ',') break;
+    }
+    if (bad) {
+        static std::once_flag warned;
+        std::call_once(warned, [e, count] {
+            fprintf(stderr,
+                    "gfx_imagecompress_amd: GIC_DEVICES=\"%s\" is not a comma-separated list of device "
+                    "indices in [0, %d); running on the current device only\n", e, count);
+        });
+        return {};
     }
     return out;
 }
 
-// Host-image driver shared by the image-level wrappers: uploads the source,
-// encodes in chunks of block rows, reports progress per block row exactly as
-// the reference loops do (amd_bc1_compressor.cpp:64-68), downloads blocks.
+// Host-image driver shared by the image-level wrappers: the block rows go
+// through the upload / encode / download pipeline (gic_pipeline.cpp) on the
+// current device, or on every device GIC_DEVICES lists; progress is reported
+// per block row exactly as the reference loops do (amd_bc1_compressor.cpp:64-68),
+// abort => NULL.
 static Image_ImageHeader const *encode_host_image(Image_ImageHeader const *src, gic_format fmt, TinyImageFormat dst_fmt,
                                                   const gic_options &o, Image_CompressProgressFunc cb, void *user)
 {
+    t_host_report = gic_host_report{};
     if (!src || !src->data || src->depth > 1) return nullptr;
     const uint32_t ch = TinyImageFormat_ChannelCount(src->format);
     if (!ch || TinyImageFormat_IsCompressed(src->format)) return nullptr;
@@ -597,66 +631,71 @@ static Image_ImageHeader const *encode_host_image(Image_ImageHeader const *src, 
                           : TinyImageFormat_IsSigned(src->format) ? GIC_SRC_SNORM8
                                                                   : GIC_SRC_UNORM8;
     const size_t texel_bytes = st == GIC_SRC_FLOAT32 ? 4 : 1;
+    if (check_options(fmt, o) != GIC_OK) return nullptr;
     Image_ImageHeader const *dst = Image_CreateNoClear(src->width, src->height, 1, src->slices, dst_fmt);
     if (!dst) return nullptr;
-    const uint32_t bx = (src->width + 3) / 4, by = (src->height + 3) / 4;
     const size_t pitch = (size_t)src->width * ch * texel_bytes;
-    const size_t src_bytes = pitch * src->height * src->slices;
-    const size_t bb = gic_block_bytes(fmt);
-    const size_t dst_bytes = (size_t)bx * by * src->slices * bb;
-    // GIC_DEVICES="0,1,..." (more than one device) and no progress callback: the
-    // block rows go over the listed devices with one gather (gic_encode_multi)
-    std::vector<int> devs;
-    if (!cb) devs = env_devices();
+    const gic::EncodeArgs args{fmt, st, src->width, src->height, ch, pitch, &o};
+    const std::vector<int> devs = env_devices();
+    int rc;
     if (devs.size() > 1) {
+        rc = gic::encode_host_devices(devs, args, (const uint8_t *)src->data, src->slices, (uint8_t *)dst->data, cb,
+                                      user, &t_host_report);
+    } else {
         int cur = 0;
-        bool ok = hipGetDevice(&cur) == hipSuccess && hipSetDevice(devs[0]) == hipSuccess;
-        uint8_t *d = nullptr;
-        ok = ok && hipMalloc((void **)&d, dst_bytes) == hipSuccess;
-        ok = ok && gic_encode_multi(fmt, st, src->data, src->width, src->height, src->slices, ch, pitch, &o,
-                                    (int)devs.size(), devs.data(), d, 0) == GIC_OK;
-        ok = ok && hipSetDevice(devs[0]) == hipSuccess &&
-             hipMemcpy(dst->data, d, dst_bytes, hipMemcpyDeviceToHost) == hipSuccess;
-        if (d) (void)hipFree(d);
+        rc = hipGetDevice(&cur) == hipSuccess && t_lane.lb.lane.init(cur) == hipSuccess ? GIC_OK : GIC_EHIP;
+        if (rc == GIC_OK)
+            rc = gic::encode_host({&t_lane.lb}, args, (const uint8_t *)src->data, src->slices, (uint8_t *)dst->data,
+                                  cb, user, &t_host_report);
         (void)hipSetDevice(cur);
-        if (!ok) {
-            fprintf(stderr, "gfx_imagecompress_amd: multi-GPU encode failed\n");
-            Image_Destroy(dst);
-            return nullptr;
-        }
-        return dst;
     }
-    DeviceScratch &s = t_scratch;
-    bool ok = s.reserve(src_bytes, dst_bytes) &&
-              hipMemcpyAsync(s.src, src->data, src_bytes, hipMemcpyHostToDevice, s.stream) == hipSuccess;
-    const uint32_t chunk = cb ? 16u : by;   // rows per launch when reporting progress
-    for (uint32_t w = 0; ok && w < src->slices; ++w) {
-        const uint8_t *slice_src = (const uint8_t *)s.src + pitch * src->height * w;
-        uint8_t *slice_dst = (uint8_t *)s.dst + (size_t)bx * by * bb * w;
-        for (uint32_t y0 = 0; ok && y0 < by; y0 += chunk) {
-            const uint32_t n = (by - y0) < chunk ? (by - y0) : chunk;
-            ok = gic_hip_encode_rows_src(fmt, st, slice_src, src->width, src->height, 1, ch, pitch, y0, n, &o,
-                                         slice_dst + (size_t)y0 * bx * bb, nullptr, s.stream) == GIC_OK;
-            if (ok && cb) {
-                ok = hipStreamSynchronize(s.stream) == hipSuccess;
-                for (uint32_t y = y0; ok && y < y0 + n; ++y) {
-                    const float pct = 100.f * (y * bx) / (bx * by);
-                    if (cb(user, pct)) {   // abort requested
-                        Image_Destroy(dst);
-                        return nullptr;
-                    }
-                }
-            }
-        }
-    }
-    ok = ok && hipMemcpyAsync(dst->data, s.dst, dst_bytes, hipMemcpyDeviceToHost, s.stream) == hipSuccess &&
-         hipStreamSynchronize(s.stream) == hipSuccess;
-    if (!ok) {
-        fprintf(stderr, "gfx_imagecompress_amd: GPU encode failed (HIP error %d)\n", (int)hipGetLastError());
+    if (rc != GIC_OK) {
+        if (rc != GIC_EABORT)
+            fprintf(stderr, "gfx_imagecompress_amd: GPU encode failed (%d, HIP error %d)\n", rc, gic_last_hip_error());
         Image_Destroy(dst);
         return nullptr;
     }
     return dst;
+}
+
+extern "C" int gic_last_host_report(gic_host_report *out)
+{
+    if (!out) return GIC_EINVAL;
+    *out = t_host_report;
+    return GIC_OK;
+}
+
+extern "C" Image_ImageHeader const *gic_compress_image(Image_ImageHeader const *src, gic_format fmt,
+                                                       const gic_options *opt, bool (*progress)(void *, float),
+                                                       void *user)
+{
+    if (!src || !valid_fmt(fmt)) return nullptr;
+    gic_options o;
+    gic_default_options(&o);
+    if (opt) {
+        if (opt->struct_size != sizeof(gic_options)) return nullptr;
+        o = *opt;
+    }
+    const bool srgb = TinyImageFormat_IsSRGB(src->format), sgn = TinyImageFormat_IsSigned(src->format);
+    const bool alpha = TinyImageFormat_ChannelCount(src->format) > 3;
+    if (!alpha) o.force_alpha_one = 1;
+    TinyImageFormat f = TinyImageFormat_UNDEFINED;
+    switch (fmt) {
+    case GIC_FMT_BC1:
+        f = alpha ? (srgb ? TinyImageFormat_DXBC1_RGBA_SRGB : TinyImageFormat_DXBC1_RGBA_UNORM)
+                  : (srgb ? TinyImageFormat_DXBC1_RGB_SRGB : TinyImageFormat_DXBC1_RGB_UNORM);
+        break;
+    case GIC_FMT_BC2: f = srgb ? TinyImageFormat_DXBC2_SRGB : TinyImageFormat_DXBC2_UNORM; break;
+    case GIC_FMT_BC3: f = srgb ? TinyImageFormat_DXBC3_SRGB : TinyImageFormat_DXBC3_UNORM; break;
+    case GIC_FMT_BC4: f = sgn ? TinyImageFormat_DXBC4_SNORM : TinyImageFormat_DXBC4_UNORM; break;
+    case GIC_FMT_BC5: f = sgn ? TinyImageFormat_DXBC5_SNORM : TinyImageFormat_DXBC5_UNORM; break;
+    case GIC_FMT_BC7:
+    case GIC_FMT_BC7ENC16: f = srgb ? TinyImageFormat_DXBC7_SRGB : TinyImageFormat_DXBC7_UNORM; break;
+    case GIC_FMT_BC6H: f = TinyImageFormat_DXBC6H_UFLOAT; break;
+    case GIC_FMT_BC6H_SF: f = TinyImageFormat_DXBC6H_SFLOAT; break;
+    default: return nullptr;
+    }
+    return encode_host_image(src, fmt, f, o, progress, user);
 }
 
 static Image_CompressAMDBackendOptions const kDefaultAmd = {false, false, 1, 0xFF};   // amd_bcx_helpers.cpp:23-31

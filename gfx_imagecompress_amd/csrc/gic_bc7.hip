@@ -3296,6 +3296,10 @@ static void base_params(const gic_options &o, const DeviceState &st, double perf
 
 // H4 report of the calling thread's last BC7 call (gic_last_h4_report)
 thread_local uint32_t t_h4_rerun = 0, t_h4_nonterm = 0;
+// blocks entering each stage of the calling thread's last BC7 call
+// (gic_last_bc7_stages): bounded exit = probe 6, probe 3, probe 1, search
+thread_local uint32_t t_stage_in[4] = {0, 0, 0, 0};
+thread_local int t_nstages = 0;
 
 static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t total, const gic_options &o, void *dst,
                              double *err, hipStream_t s)
@@ -3390,8 +3394,11 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
     const uint32_t *cur = nullptr;
     uint32_t cur_n = total;
     uint32_t ci = 0;
+    for (int k = 0; k < 4; ++k) t_stage_in[k] = 0;
+    t_nstages = nstages;
     for (int si = 0; si < nstages && cur_n; ++si) {
         const int pk = stages[si];
+        t_stage_in[si] = cur_n;
         const bool last_stage = si == nstages - 1;
         uint32_t *out = bounded ? st->list[si & 1] : nullptr;
         for (uint32_t first = 0; first < cur_n; first += chunk, ++ci) {
@@ -3569,6 +3576,12 @@ hipError_t bc7_nonterm(unsigned long long *n, int reset)
         if (e == hipSuccess) bc7::g_states[dev].nonterm_seen = 0;
     }
     return e;
+}
+
+void bc7_last_stages(uint32_t in[4], int *n)
+{
+    for (int k = 0; k < 4; ++k) in[k] = bc7::t_stage_in[k];
+    *n = bc7::t_nstages;
 }
 
 void bc7_last_h4(uint32_t *rerun, uint32_t *nonterm)

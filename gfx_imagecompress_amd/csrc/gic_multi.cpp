@@ -1,4 +1,5 @@
-// gic_multi.cpp -- multi-GPU encode from one host process behind the C ABI.
+// gic_multi.cpp -- multi-GPU encode from one host process behind the C ABI,
+// and the lane driver shared with the host-image entry points.
 //
 // SURVEY.md 8(e) / north_star: "images shard by block-row across the GPUs of
 // one node with a single RCCL gather of the packed BCn bitstream over xGMI at
@@ -8,40 +9,105 @@
 // numbered slice-major, are cut into one contiguous range per device, so each
 // device's packed blocks form one contiguous piece of the reference-ordered
 // output.  Per device (one host thread each, so BC7 calls -- which return with
-// their device work complete, gic_bc7.hip H4 -- overlap across devices):
-// upload the source rows its range reads, encode them with the row-range entry
-// (gic_hip_encode_rows_src) on its own stream.  Then one gather: grouped
-// ncclSend / ncclRecv over communicators from ncclCommInitAll (built once per
-// device list) lands every piece at its offset in the root's buffer; the root's
-// own piece is encoded in place.  A list that names a device twice cannot form
-// an RCCL communicator; it gathers with peer copies instead (the one-GPU test
-// path of the same split).
+// their device work complete, gic_bc7.hip H4 -- overlap across devices) the
+// range runs through the upload / encode pipeline of gic_pipeline.cpp, and as
+// soon as a device's last piece is encoded its blocks go to their offset in
+// the root's buffer: ncclSend on the device's comm, matched by ncclRecv posted
+// up front on a gather stream of the root (communicators from ncclCommInitAll
+// over the list, built once per list), so the gather of a fast device overlaps
+// the slower devices' encodes.  The root's own piece is encoded in place.  A
+// list that names a device twice cannot form an RCCL communicator; it gathers
+// with peer copies instead (the one-GPU test path of the same split).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
 
 #include "gfx_imagecompress_amd/gic.h"
+#include "gic_pipeline.h"
+
+namespace gic {
+
+double now_ms()
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int drive(std::vector<LaneJob> &jobs, const EncodeArgs &a, uint32_t bx, uint32_t by, ProgressFn cb, void *user)
+{
+    Progress prog;
+    prog.done.assign(jobs.size(), 0);
+    auto run = [&](int i) {
+        LaneJob &j = jobs[i];
+        const double t0 = now_ms();
+        j.rc = run_pieces(*j.lane, a, j.pieces, &prog, i, &j.times);
+        if (j.rc == GIC_OK && j.after && !prog.abort.load()) j.rc = j.after();
+        j.wall_ms = now_ms() - t0;
+        if (j.rc != GIC_OK) prog.abort.store(true);   // the other lanes stop between pieces
+        prog.finish();
+    };
+    bool aborted = false;
+    if (jobs.size() == 1 && !cb) {
+        run(0);
+    } else {
+        std::vector<std::thread> th;
+        for (size_t i = 0; i < jobs.size(); ++i) th.emplace_back(run, (int)i);
+        if (cb) {
+            // rows in slice-major order; row g belongs to the job whose range holds it
+            uint64_t total = 0;
+            for (const LaneJob &j : jobs) total = j.first_row + j.rows > total ? j.first_row + j.rows : total;
+            size_t owner = 0;
+            for (uint64_t g = 0; g < total && !aborted;) {
+                while (owner < jobs.size() && g >= jobs[owner].first_row + jobs[owner].rows) ++owner;
+                if (owner == jobs.size()) break;
+                {
+                    std::unique_lock<std::mutex> lk(prog.m);
+                    prog.cv.wait(lk, [&] {
+                        return g < jobs[owner].first_row + prog.done[owner] || prog.finished == (int)jobs.size();
+                    });
+                    if (g >= jobs[owner].first_row + prog.done[owner]) break;   // a lane failed
+                }
+                const uint64_t ready = jobs[owner].first_row + [&] {
+                    std::lock_guard<std::mutex> lk(prog.m);
+                    return prog.done[owner];
+                }();
+                for (; g < ready; ++g) {
+                    const uint32_t y = (uint32_t)(g % by);
+                    const float pct = 100.f * (y * bx) / (bx * by);
+                    if (cb(user, pct)) {
+                        aborted = true;
+                        prog.abort.store(true);
+                        break;
+                    }
+                }
+            }
+        }
+        for (std::thread &t : th) t.join();
+    }
+    if (aborted) return GIC_EABORT;
+    for (const LaneJob &j : jobs)
+        if (j.rc != GIC_OK) return j.rc;
+    return GIC_OK;
+}
+
+}  // namespace gic
 
 namespace {
 
-struct Rank {
-    int device = -1;
-    hipStream_t stream = nullptr;
-    hipEvent_t done = nullptr;
-    uint8_t *src = nullptr, *dst = nullptr;
-    size_t src_cap = 0, dst_cap = 0;
-};
+using Rank = gic::LaneBuffers;
 
 struct Group {
     std::vector<int> devices;
-    std::vector<Rank> ranks;
+    std::vector<std::unique_ptr<Rank>> ranks;
     std::vector<ncclComm_t> comms;   // empty: peer copies
+    hipStream_t gather = nullptr;    // the root's receive stream (RCCL)
     bool rccl = false, tried = false;
 };
 
@@ -59,14 +125,12 @@ void release(Group &g)
 {
     for (ncclComm_t c : g.comms) (void)ncclCommDestroy(c);
     g.comms.clear();
-    for (Rank &r : g.ranks) {
-        if (r.device < 0) continue;
-        (void)hipSetDevice(r.device);
-        if (r.src) (void)hipFree(r.src);
-        if (r.dst) (void)hipFree(r.dst);
-        if (r.done) (void)hipEventDestroy(r.done);
-        if (r.stream) (void)hipStreamDestroy(r.stream);
+    if (g.gather && !g.ranks.empty()) {
+        (void)hipSetDevice(g.ranks[0]->lane.device);
+        (void)hipStreamDestroy(g.gather);
     }
+    g.gather = nullptr;
+    for (auto &r : g.ranks) r->release();
     g.ranks.clear();
     g.devices.clear();
     g.rccl = g.tried = false;
@@ -79,17 +143,19 @@ hipError_t get_group(int ndev, const int *devices, bool want_rccl, Group *&out)
     if (g_group.devices != want) {
         release(g_group);
         g_group.devices = want;
-        g_group.ranks.resize(ndev);
         for (int i = 0; i < ndev; ++i) {
-            Rank &r = g_group.ranks[i];
-            r.device = devices[i];
-            hipError_t e = hipSetDevice(r.device);
-            if (e == hipSuccess) e = hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&r.done, hipEventDisableTiming);
+            g_group.ranks.emplace_back(new Rank);
+            const hipError_t e = g_group.ranks.back()->lane.init(devices[i]);
             if (e != hipSuccess) {
                 release(g_group);
                 return e;
             }
+        }
+        hipError_t e = hipSetDevice(devices[0]);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&g_group.gather, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            release(g_group);
+            return e;
         }
     }
     bool distinct = true;
@@ -97,14 +163,12 @@ hipError_t get_group(int ndev, const int *devices, bool want_rccl, Group *&out)
         for (int j = i + 1; j < ndev; ++j) distinct = distinct && devices[i] != devices[j];
     if (want_rccl && distinct && ndev > 1 && !g_group.tried) {
         g_group.tried = true;
-        {
-            g_group.comms.resize(ndev);
-            if (ncclCommInitAll(g_group.comms.data(), ndev, devices) == ncclSuccess) {
-                g_group.rccl = true;
-            } else {
-                g_group.comms.clear();
-                fprintf(stderr, "gfx_imagecompress_amd: ncclCommInitAll failed; gathering with peer copies\n");
-            }
+        g_group.comms.resize(ndev);
+        if (ncclCommInitAll(g_group.comms.data(), ndev, devices) == ncclSuccess) {
+            g_group.rccl = true;
+        } else {
+            g_group.comms.clear();
+            fprintf(stderr, "gfx_imagecompress_amd: ncclCommInitAll failed; gathering with peer copies\n");
         }
     }
     out = &g_group;
@@ -121,6 +185,8 @@ hipError_t grow(uint8_t *&p, size_t &cap, size_t need)
     if (e == hipSuccess) cap = need;
     return e;
 }
+
+bool valid_source(gic_source st) { return st == GIC_SRC_UNORM8 || st == GIC_SRC_SNORM8 || st == GIC_SRC_FLOAT32; }
 
 }  // namespace
 
@@ -141,8 +207,7 @@ extern "C" int gic_encode_multi(gic_format fmt, gic_source src_type, const void 
                                 uint32_t flags)
 {
     if (!h_src || !d_dst_root || !width || !height || !slices || channels < 1 || channels > 4) return GIC_EINVAL;
-    if (ndev < 1 || ndev > 64 || !devices) return GIC_EINVAL;
-    if (src_type != GIC_SRC_UNORM8 && src_type != GIC_SRC_SNORM8 && src_type != GIC_SRC_FLOAT32) return GIC_EINVAL;
+    if (ndev < 1 || ndev > 64 || !devices || !valid_source(src_type)) return GIC_EINVAL;
     const size_t texel = (size_t)channels * (src_type == GIC_SRC_FLOAT32 ? 4 : 1);
     if (row_pitch < (size_t)width * texel) return GIC_EINVAL;
     const uint32_t bb = gic_block_bytes(fmt);
@@ -154,140 +219,182 @@ extern "C" int gic_encode_multi(gic_format fmt, gic_source src_type, const void 
     const uint32_t bx = (width + 3) / 4, by = (height + 3) / 4;
     const uint64_t rows_total = (uint64_t)by * slices;
     const size_t row_bytes = (size_t)bx * bb;   // packed blocks of one block row
-    const size_t slice_bytes = row_pitch * height;
 
     std::lock_guard<std::mutex> lk(g_multi_lock);
     DeviceGuard guard;
     Group *g = nullptr;
-    hipError_t e = get_group(ndev, devices, !(flags & GIC_MULTI_PEER_COPY), g);
-    if (e != hipSuccess) return GIC_EHIP;
+    if (get_group(ndev, devices, !(flags & GIC_MULTI_PEER_COPY), g) != hipSuccess) return GIC_EHIP;
     const bool rccl = g->rccl && !(flags & GIC_MULTI_PEER_COPY);
-
-    std::vector<uint64_t> first(ndev), nrows(ndev);
-    for (int i = 0; i < ndev; ++i) gic_multi_split(rows_total, ndev, i, &first[i], &nrows[i]);
     t_report = gic_multi_report{};
     t_report.ranks = ndev;
     t_report.rccl = rccl ? 1 : 0;
 
-    std::vector<int> rc(ndev, GIC_OK);
-    std::vector<hipError_t> he(ndev, hipSuccess);
-    std::vector<double> enc_ms(ndev, 0.0);
-    auto encode_rank = [&](int i) {
-        Rank &r = g->ranks[i];
-        hipError_t err = hipSetDevice(r.device);
-        if (err != hipSuccess || !nrows[i]) {
-            he[i] = err;
-            return;
-        }
-        // the slice segments of the range and the source bytes they read
-        struct Seg {
-            uint32_t slice, y0, y1;
-            size_t off;   // into the rank's source slab
-        };
-        std::vector<Seg> segs;
-        size_t slab = 0;
-        for (uint64_t row = first[i], end = first[i] + nrows[i]; row < end;) {
-            const uint32_t w = (uint32_t)(row / by), y0 = (uint32_t)(row % by);
-            const uint32_t y1 = (uint32_t)((end - (uint64_t)w * by) < by ? (end - (uint64_t)w * by) : by);
-            const uint32_t py1 = 4 * y1 < height ? 4 * y1 : height;
-            segs.push_back({w, y0, y1, slab});
-            slab += (size_t)(py1 - 4 * y0) * row_pitch;
-            row = (uint64_t)w * by + y1;
-        }
-        const bool root = i == 0;
-        err = grow(r.src, r.src_cap, slab);
-        if (err == hipSuccess && !root) err = grow(r.dst, r.dst_cap, nrows[i] * row_bytes);
-        hipEvent_t t0 = nullptr, t1 = nullptr;
-        if (err == hipSuccess) err = hipEventCreate(&t0);
-        if (err == hipSuccess) err = hipEventCreate(&t1);
-        if (err == hipSuccess) err = hipEventRecord(t0, r.stream);
-        for (const Seg &sg : segs) {
-            if (err != hipSuccess) break;
-            const uint32_t py1 = 4 * sg.y1 < height ? 4 * sg.y1 : height;
-            const uint8_t *hs = (const uint8_t *)h_src + slice_bytes * sg.slice + (size_t)4 * sg.y0 * row_pitch;
-            err = hipMemcpyAsync(r.src + sg.off, hs, (size_t)(py1 - 4 * sg.y0) * row_pitch, hipMemcpyHostToDevice,
-                                 r.stream);
-        }
-        size_t out_off = 0;
-        for (const Seg &sg : segs) {
-            if (err != hipSuccess) break;
-            // the slab holds pixel rows [4 y0, ...) of the slice: address it as the
-            // whole slice (the kernels read only rows of block rows y0..y1-1, and
-            // the edge clamp of the image's last block row stays inside the slab)
-            const uint8_t *base = r.src + sg.off - (size_t)4 * sg.y0 * row_pitch;
-            uint8_t *out = root ? d_dst_root + first[i] * row_bytes + out_off : r.dst + out_off;
-            rc[i] = gic_hip_encode_rows_src(fmt, src_type, base, width, height, 1, channels, row_pitch, sg.y0,
-                                            sg.y1 - sg.y0, opt, out, nullptr, r.stream);
-            if (rc[i] != GIC_OK) break;
-            out_off += (size_t)(sg.y1 - sg.y0) * row_bytes;
-        }
-        if (err == hipSuccess) err = hipEventRecord(t1, r.stream);
-        if (err == hipSuccess) err = hipEventRecord(r.done, r.stream);
-        if (err == hipSuccess) err = hipStreamSynchronize(r.stream);
-        float ms = 0.f;
-        if (err == hipSuccess && hipEventElapsedTime(&ms, t0, t1) == hipSuccess) enc_ms[i] = ms;
-        if (t0) (void)hipEventDestroy(t0);
-        if (t1) (void)hipEventDestroy(t1);
-        he[i] = err;
-    };
-    {
-        std::vector<std::thread> th;
-        for (int i = 1; i < ndev; ++i) th.emplace_back(encode_rank, i);
-        encode_rank(0);
-        for (std::thread &t : th) t.join();
-    }
+    const gic::EncodeArgs args{fmt, src_type, width, height, channels, row_pitch, opt};
+    const uint32_t per = gic::piece_rows(fmt, bx);
+    std::vector<gic::LaneJob> jobs(ndev);
+    std::vector<double> encoded_at(ndev, 0.0);
+    const double t0 = gic::now_ms();
     for (int i = 0; i < ndev; ++i) {
-        if (rc[i] != GIC_OK) return rc[i];
-        if (he[i] != hipSuccess) return GIC_EHIP;
-        t_report.encode_ms_max = enc_ms[i] > t_report.encode_ms_max ? enc_ms[i] : t_report.encode_ms_max;
+        Rank &r = *g->ranks[i];
+        uint64_t first = 0, n = 0;
+        gic_multi_split(rows_total, ndev, i, &first, &n);
+        gic::LaneJob &j = jobs[i];
+        j.lane = &r.lane;
+        j.first_row = first;
+        j.rows = n;
+        if (!n) continue;
+        if (hipSetDevice(r.lane.device) != hipSuccess) return GIC_EHIP;
+        if (grow(r.src, r.src_cap, gic::slab_bytes(first, n, by, height, row_pitch)) != hipSuccess) return GIC_EHIP;
+        if (i && grow(r.dst, r.dst_cap, n * row_bytes) != hipSuccess) return GIC_EHIP;
+        uint8_t *out = i ? r.dst : d_dst_root + first * row_bytes;
+        j.pieces = gic::make_pieces(first, n, per, by, height, row_pitch, row_bytes, (const uint8_t *)h_src, r.src,
+                                    out, nullptr);
+        if (!i) {
+            j.after = [&, i] {
+                encoded_at[i] = gic::now_ms();
+                return GIC_OK;
+            };
+            continue;
+        }
+        // the device's blocks go to the root as soon as its last piece is encoded
+        j.after = [&, i, first, n] {
+            Rank &rr = *g->ranks[i];
+            encoded_at[i] = gic::now_ms();
+            const size_t bytes = n * row_bytes;
+            hipError_t e = hipSuccess;
+            if (rccl) {
+                const ncclResult_t nr = ncclSend(rr.dst, bytes, ncclUint8, 0, g->comms[i], rr.lane.enc);
+                if (nr != ncclSuccess) {
+                    fprintf(stderr, "gfx_imagecompress_amd: RCCL send failed (%s)\n", ncclGetErrorString(nr));
+                    return GIC_EHIP;
+                }
+            } else {
+                e = hipMemcpyPeerAsync(d_dst_root + first * row_bytes, g->ranks[0]->lane.device, rr.dst,
+                                       rr.lane.device, bytes, rr.lane.enc);
+            }
+            if (e == hipSuccess) e = hipStreamSynchronize(rr.lane.enc);
+            return e == hipSuccess ? GIC_OK : GIC_EHIP;
+        };
     }
-
-    // the gather: every non-root piece to its offset in the root's buffer
-    Rank &root = g->ranks[0];
-    hipEvent_t g0 = nullptr, g1 = nullptr;
-    e = hipSetDevice(root.device);
-    if (e == hipSuccess) e = hipEventCreate(&g0);
-    if (e == hipSuccess) e = hipEventCreate(&g1);
-    if (e == hipSuccess) e = hipEventRecord(g0, root.stream);
-    if (e != hipSuccess) return GIC_EHIP;
+    // RCCL: the root's receives are posted up front on its gather stream, in
+    // rank order, before the senders start (each pair has one send / recv)
+    std::thread receiver;
+    int recv_rc = GIC_OK;
     if (rccl) {
-        ncclResult_t nr = ncclGroupStart();
-        for (int i = 1; i < ndev && nr == ncclSuccess; ++i) {
-            if (!nrows[i]) continue;
-            const size_t n = nrows[i] * row_bytes;
-            nr = ncclSend(g->ranks[i].dst, n, ncclUint8, 0, g->comms[i], g->ranks[i].stream);
-            if (nr == ncclSuccess)
-                nr = ncclRecv(d_dst_root + first[i] * row_bytes, n, ncclUint8, i, g->comms[0], root.stream);
-        }
-        const ncclResult_t ne = ncclGroupEnd();
-        if (nr != ncclSuccess || ne != ncclSuccess) {
-            fprintf(stderr, "gfx_imagecompress_amd: RCCL gather failed (%s)\n",
-                    ncclGetErrorString(nr != ncclSuccess ? nr : ne));
-            return GIC_EHIP;
-        }
-    } else {
-        for (int i = 1; i < ndev && e == hipSuccess; ++i) {
-            if (!nrows[i]) continue;
-            const size_t n = nrows[i] * row_bytes;
-            e = hipMemcpyPeerAsync(d_dst_root + first[i] * row_bytes, root.device, g->ranks[i].dst,
-                                   g->ranks[i].device, n, root.stream);
-        }
+        receiver = std::thread([&] {
+            (void)hipSetDevice(g->ranks[0]->lane.device);
+            for (int i = 1; i < ndev && recv_rc == GIC_OK; ++i) {
+                if (!jobs[i].rows) continue;
+                const ncclResult_t nr = ncclRecv(d_dst_root + jobs[i].first_row * row_bytes, jobs[i].rows * row_bytes,
+                                                 ncclUint8, i, g->comms[0], g->gather);
+                if (nr != ncclSuccess) {
+                    fprintf(stderr, "gfx_imagecompress_amd: RCCL receive failed (%s)\n", ncclGetErrorString(nr));
+                    recv_rc = GIC_EHIP;
+                }
+            }
+            if (recv_rc == GIC_OK && hipStreamSynchronize(g->gather) != hipSuccess) recv_rc = GIC_EHIP;
+        });
     }
-    if (e == hipSuccess) e = hipEventRecord(g1, root.stream);
-    for (int i = 0; i < ndev && e == hipSuccess; ++i) {
-        e = hipSetDevice(g->ranks[i].device);
-        if (e == hipSuccess) e = hipStreamSynchronize(g->ranks[i].stream);
+    int rc = gic::drive(jobs, args, bx, by, nullptr, nullptr);
+    if (rc != GIC_OK && rccl) {
+        // a device failed before its send: the root's posted receive would wait
+        // forever, so the communicators are aborted (rebuilt by the next call)
+        for (ncclComm_t c : g->comms) (void)ncclCommAbort(c);
+        g->comms.clear();
+        g->rccl = g->tried = false;
     }
-    float gms = 0.f;
-    if (e == hipSuccess) e = hipEventElapsedTime(&gms, g0, g1);
-    (void)hipSetDevice(root.device);
-    (void)hipEventDestroy(g0);
-    (void)hipEventDestroy(g1);
-    if (e != hipSuccess) return GIC_EHIP;
-    t_report.gather_ms = gms;
-    for (int i = 1; i < ndev; ++i) t_report.gathered_bytes += nrows[i] * row_bytes;
+    if (receiver.joinable()) receiver.join();
+    const double t1 = gic::now_ms();
+    if (rc == GIC_OK) rc = recv_rc;
+    if (rc != GIC_OK) return rc;
+    double last_encoded = 0.0;
+    for (int i = 0; i < ndev; ++i) {
+        if (!jobs[i].rows) continue;
+        const double enc = encoded_at[i] - t0;
+        t_report.encode_ms_max = enc > t_report.encode_ms_max ? enc : t_report.encode_ms_max;
+        last_encoded = encoded_at[i] > last_encoded ? encoded_at[i] : last_encoded;
+        if (i) t_report.gathered_bytes += jobs[i].rows * row_bytes;
+    }
+    // the gather's exposed part: from the last device's encode to the end of the call
+    t_report.gather_ms = t1 - last_encoded > 0 ? t1 - last_encoded : 0.0;
     return GIC_OK;
 }
+
+namespace gic {
+
+hipError_t LaneBuffers::reserve(size_t src_bytes, size_t dst_bytes)
+{
+    hipError_t e = hipSetDevice(lane.device);
+    if (e == hipSuccess) e = grow(src, src_cap, src_bytes);
+    if (e == hipSuccess) e = grow(dst, dst_cap, dst_bytes);
+    return e;
+}
+
+void LaneBuffers::release()
+{
+    if (lane.device >= 0) {
+        (void)hipSetDevice(lane.device);
+        if (src) (void)hipFree(src);
+        if (dst) (void)hipFree(dst);
+    }
+    src = dst = nullptr;
+    src_cap = dst_cap = 0;
+    lane.release();
+}
+
+int encode_host(const std::vector<LaneBuffers *> &lanes, const EncodeArgs &a, const uint8_t *h_src, uint32_t slices,
+                uint8_t *h_out, ProgressFn cb, void *user, gic_host_report *rep)
+{
+    const double t0 = now_ms();
+    const uint32_t bb = gic_block_bytes(a.fmt);
+    const uint32_t bx = (a.width + 3) / 4, by = (a.height + 3) / 4;
+    const uint64_t rows_total = (uint64_t)by * slices;
+    const size_t row_bytes = (size_t)bx * bb;
+    const int n = (int)lanes.size();
+    const uint32_t per = piece_rows(a.fmt, bx);
+    std::vector<LaneJob> jobs(n);
+    for (int i = 0; i < n; ++i) {
+        uint64_t first = 0, rows = 0;
+        gic_multi_split(rows_total, n, i, &first, &rows);
+        LaneJob &j = jobs[i];
+        j.lane = &lanes[i]->lane;
+        j.first_row = first;
+        j.rows = rows;
+        if (!rows) continue;
+        if (lanes[i]->reserve(slab_bytes(first, rows, by, a.height, a.row_pitch), rows * row_bytes) != hipSuccess)
+            return GIC_EHIP;
+        j.pieces = make_pieces(first, rows, per, by, a.height, a.row_pitch, row_bytes, h_src, lanes[i]->src,
+                               lanes[i]->dst, h_out + first * row_bytes);
+    }
+    const int rc = drive(jobs, a, bx, by, cb, user);
+    if (rep) {
+        *rep = gic_host_report{};
+        rep->devices = n;
+        rep->h2d_mode = (int)h2d_mode();
+        rep->total_ms = now_ms() - t0;
+        for (const LaneJob &j : jobs) {
+            rep->pieces += (int)j.pieces.size();
+            rep->h2d_ms = j.times.h2d_ms > rep->h2d_ms ? j.times.h2d_ms : rep->h2d_ms;
+            rep->encode_ms = j.times.encode_ms > rep->encode_ms ? j.times.encode_ms : rep->encode_ms;
+            rep->d2h_ms = j.times.d2h_ms > rep->d2h_ms ? j.times.d2h_ms : rep->d2h_ms;
+        }
+    }
+    return rc;
+}
+
+int encode_host_devices(const std::vector<int> &devices, const EncodeArgs &a, const uint8_t *h_src, uint32_t slices,
+                        uint8_t *h_out, ProgressFn cb, void *user, gic_host_report *rep)
+{
+    std::lock_guard<std::mutex> lk(g_multi_lock);
+    DeviceGuard guard;
+    Group *g = nullptr;
+    if (get_group((int)devices.size(), devices.data(), false, g) != hipSuccess) return GIC_EHIP;
+    std::vector<LaneBuffers *> lanes;
+    for (auto &r : g->ranks) lanes.push_back(r.get());
+    return encode_host(lanes, a, h_src, slices, h_out, cb, user, rep);
+}
+
+}  // namespace gic
 
 extern "C" int gic_multi_last_report(gic_multi_report *out)
 {

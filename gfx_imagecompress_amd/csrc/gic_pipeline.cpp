@@ -1,0 +1,313 @@
+// gic_pipeline.cpp -- upload / encode / download overlap for host images
+// (see gic_pipeline.h).
+#include "gic_pipeline.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+
+namespace gic {
+
+H2D h2d_mode()
+{
+    const char *e = getenv("GIC_H2D");   // read per call: a process may compare modes
+    if (!e || !*e || !strcmp(e, "pageable")) return H2D::Pageable;
+    if (!strcmp(e, "staged")) return H2D::Staged;
+    if (!strcmp(e, "register")) return H2D::Register;
+    static std::once_flag warned;
+    std::call_once(warned, [e] {
+        fprintf(stderr, "gfx_imagecompress_amd: GIC_H2D=%s not understood (pageable | staged | register); "
+                        "using pageable\n", e);
+    });
+    return H2D::Pageable;
+}
+
+static constexpr int kStageSlots = 3;
+
+hipError_t Lane::init(int dev)
+{
+    if (device == dev && up) return hipSuccess;
+    release();
+    device = dev;
+    hipError_t e = hipSetDevice(dev);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&up, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&enc, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&down, hipStreamNonBlocking);
+    for (hipEvent_t *t : {&t_up0, &t_up1, &t_enc0, &t_enc1, &t_dn0, &t_dn1})
+        if (e == hipSuccess) e = hipEventCreate(t);
+    if (e != hipSuccess) release();
+    return e;
+}
+
+hipError_t Lane::reserve_events(size_t pieces)
+{
+    hipError_t e = hipSuccess;
+    while (e == hipSuccess && ev_up.size() < pieces) {
+        hipEvent_t a = nullptr, b = nullptr;
+        e = hipEventCreateWithFlags(&a, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&b, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            if (a) (void)hipEventDestroy(a);
+            break;
+        }
+        ev_up.push_back(a);
+        ev_enc.push_back(b);
+    }
+    return e;
+}
+
+hipError_t Lane::reserve_stage(size_t slot_bytes)
+{
+    if (slot_bytes <= stage_slot) return hipSuccess;
+    if (stage) (void)hipHostFree(stage);
+    stage = nullptr;
+    stage_slot = 0;
+    const hipError_t e = hipHostMalloc((void **)&stage, slot_bytes * kStageSlots, hipHostMallocDefault);
+    if (e == hipSuccess) stage_slot = slot_bytes;
+    return e;
+}
+
+void Lane::release()
+{
+    if (device >= 0) (void)hipSetDevice(device);
+    for (hipEvent_t ev : ev_up) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : ev_enc) (void)hipEventDestroy(ev);
+    ev_up.clear();
+    ev_enc.clear();
+    for (hipEvent_t *t : {&t_up0, &t_up1, &t_enc0, &t_enc1, &t_dn0, &t_dn1}) {
+        if (*t) (void)hipEventDestroy(*t);
+        *t = nullptr;
+    }
+    for (hipStream_t *s : {&up, &enc, &down}) {
+        if (*s) (void)hipStreamDestroy(*s);
+        *s = nullptr;
+    }
+    if (stage) (void)hipHostFree(stage);
+    stage = nullptr;
+    stage_slot = 0;
+    device = -1;
+}
+
+uint32_t piece_rows(gic_format fmt, uint32_t blocks_x)
+{
+    uint64_t target = fmt == GIC_FMT_BC7 ? (1u << 20) : (1u << 18);
+    const char *e = getenv("GIC_PIECE_BLOCKS");   // test / tuning hook
+    if (e && atoll(e) > 0) target = (uint64_t)atoll(e);
+    const uint64_t r = target / (blocks_x ? blocks_x : 1);
+    return r < 1 ? 1u : (r > 0xffffffffull ? 0xffffffffu : (uint32_t)r);
+}
+
+size_t slab_bytes(uint64_t first, uint64_t rows, uint32_t by, uint32_t height, size_t pitch)
+{
+    size_t bytes = 0;
+    for (uint64_t row = first, end = first + rows; row < end;) {
+        const uint64_t w = row / by;
+        const uint32_t y0 = (uint32_t)(row % by);
+        const uint64_t y1 = (end - w * by) < by ? (end - w * by) : by;
+        const uint32_t py1 = 4 * y1 < height ? (uint32_t)(4 * y1) : height;
+        bytes += (size_t)(py1 - 4 * y0) * pitch;
+        row = w * by + y1;
+    }
+    return bytes;
+}
+
+std::vector<Piece> make_pieces(uint64_t first, uint64_t rows, uint32_t per, uint32_t by, uint32_t height,
+                               size_t pitch, size_t row_bytes, const uint8_t *h_src, uint8_t *d_slab, uint8_t *d_out,
+                               uint8_t *h_out)
+{
+    std::vector<Piece> out;
+    const size_t slice_bytes = pitch * height;
+    size_t off = 0;
+    for (uint64_t row = first, end = first + rows; row < end;) {
+        const uint32_t w = (uint32_t)(row / by), y0 = (uint32_t)(row % by);
+        uint64_t n = by - y0;
+        if (n > per) n = per;
+        if (n > end - row) n = end - row;
+        const uint32_t py1 = 4 * (y0 + n) < height ? (uint32_t)(4 * (y0 + n)) : height;
+        Piece p;
+        p.slice = w;
+        p.y0 = y0;
+        p.n = (uint32_t)n;
+        p.h_src = h_src + slice_bytes * w + (size_t)4 * y0 * pitch;
+        p.src_bytes = (size_t)(py1 - 4 * y0) * pitch;
+        p.d_src = d_slab + off;
+        // the slab holds pixel rows [4 y0, py1) of the slice here: address it as
+        // the whole slice (the kernels read only the rows of block rows y0..y0+n-1,
+        // and the last block row's edge clamp stays inside them)
+        p.d_slice = p.d_src - (size_t)4 * y0 * pitch;
+        p.d_out = d_out + (row - first) * row_bytes;
+        p.h_out = h_out ? h_out + (row - first) * row_bytes : nullptr;
+        p.out_bytes = n * row_bytes;
+        out.push_back(p);
+        off += p.src_bytes;
+        row += n;
+    }
+    return out;
+}
+
+namespace {
+
+// A counter one stage raises and the next waits on.
+struct Handoff {
+    std::mutex m;
+    std::condition_variable cv;
+    size_t ready = 0;
+    bool failed = false;
+    void post(size_t k)
+    {
+        {
+            std::lock_guard<std::mutex> lk(m);
+            ready = k;
+        }
+        cv.notify_all();
+    }
+    void fail()
+    {
+        {
+            std::lock_guard<std::mutex> lk(m);
+            failed = true;
+        }
+        cv.notify_all();
+    }
+    // true once piece k is ready; false if the producer failed or stopped first
+    bool wait(size_t k)
+    {
+        std::unique_lock<std::mutex> lk(m);
+        cv.wait(lk, [&] { return ready > k || failed; });
+        return ready > k;
+    }
+};
+
+struct Registration {   // page-locks a host range for the call (H2D::Register)
+    void *base = nullptr;
+    hipError_t lock(const void *p, size_t bytes)
+    {
+        const uintptr_t page = 4096, a = (uintptr_t)p & ~(page - 1);
+        const size_t len = (((uintptr_t)p + bytes + page - 1) & ~(page - 1)) - a;
+        const hipError_t e = hipHostRegister((void *)a, len, hipHostRegisterDefault);
+        if (e == hipSuccess) base = (void *)a;
+        return e;
+    }
+    ~Registration()
+    {
+        if (base) (void)hipHostUnregister(base);
+    }
+};
+
+float span_ms(hipEvent_t a, hipEvent_t b)
+{
+    float ms = 0.f;
+    return hipEventElapsedTime(&ms, a, b) == hipSuccess ? ms : 0.f;
+}
+
+}  // namespace
+
+int run_pieces(Lane &lane, const EncodeArgs &a, const std::vector<Piece> &pieces, Progress *progress, int lane_index,
+               StageTimes *times)
+{
+    if (pieces.empty()) return GIC_OK;
+    hipError_t e = hipSetDevice(lane.device);
+    if (e == hipSuccess) e = lane.reserve_events(pieces.size());
+    const H2D mode = h2d_mode();
+    size_t max_src = 0;
+    for (const Piece &p : pieces) max_src = p.src_bytes > max_src ? p.src_bytes : max_src;
+    if (e == hipSuccess && mode == H2D::Staged) e = lane.reserve_stage(max_src);
+    Registration reg;
+    if (e == hipSuccess && mode == H2D::Register) {
+        // pieces of one lane read one contiguous host range (slices are stacked)
+        const uint8_t *lo = pieces.front().h_src, *hi = pieces.back().h_src + pieces.back().src_bytes;
+        e = reg.lock(lo, (size_t)(hi - lo));
+    }
+    if (e != hipSuccess) return GIC_EHIP;
+
+    Handoff uploaded, encoded;
+    hipError_t e_up = hipSuccess, e_dn = hipSuccess;
+    std::atomic<bool> halt{false};   // the encoder failed: the other stages stop too
+    auto stop = [&] { return halt.load() || (progress && progress->abort.load(std::memory_order_relaxed)); };
+
+    std::thread uploader([&] {
+        hipError_t err = hipSetDevice(lane.device);
+        if (err == hipSuccess) err = hipEventRecord(lane.t_up0, lane.up);
+        for (size_t k = 0; k < pieces.size() && err == hipSuccess && !stop(); ++k) {
+            const Piece &p = pieces[k];
+            if (mode == H2D::Staged) {
+                // slot k % kStageSlots was last DMAed by piece k - kStageSlots
+                if (k >= (size_t)kStageSlots) err = hipEventSynchronize(lane.ev_up[k - kStageSlots]);
+                uint8_t *slot = lane.stage + (k % kStageSlots) * lane.stage_slot;
+                if (err == hipSuccess) {
+                    memcpy(slot, p.h_src, p.src_bytes);
+                    err = hipMemcpyAsync(p.d_src, slot, p.src_bytes, hipMemcpyHostToDevice, lane.up);
+                }
+            } else {
+                err = hipMemcpyAsync(p.d_src, p.h_src, p.src_bytes, hipMemcpyHostToDevice, lane.up);
+            }
+            if (err == hipSuccess) err = hipEventRecord(lane.ev_up[k], lane.up);
+            if (err == hipSuccess) uploaded.post(k + 1);
+        }
+        if (err == hipSuccess) err = hipEventRecord(lane.t_up1, lane.up);
+        e_up = err;
+        uploaded.fail();   // wakes the encoder if it waits past the last posted piece
+    });
+
+    std::thread downloader([&] {
+        hipError_t err = hipSetDevice(lane.device);
+        bool first = true;
+        for (size_t k = 0; k < pieces.size() && err == hipSuccess; ++k) {
+            if (!encoded.wait(k)) break;
+            const Piece &p = pieces[k];
+            if (p.h_out) {
+                err = hipStreamWaitEvent(lane.down, lane.ev_enc[k], 0);
+                if (err == hipSuccess && first) err = hipEventRecord(lane.t_dn0, lane.down);
+                first = false;
+                if (err == hipSuccess)
+                    err = hipMemcpyAsync(p.h_out, p.d_out, p.out_bytes, hipMemcpyDeviceToHost, lane.down);
+                if (err == hipSuccess) err = hipStreamSynchronize(lane.down);
+            } else {
+                err = hipEventSynchronize(lane.ev_enc[k]);
+            }
+            if (err == hipSuccess && progress) progress->add(lane_index, p.n);
+        }
+        if (err == hipSuccess && !first) err = hipEventRecord(lane.t_dn1, lane.down);
+        if (err == hipSuccess && !first) err = hipStreamSynchronize(lane.down);
+        e_dn = err;
+    });
+
+    int rc = GIC_OK;
+    size_t issued = 0;
+    for (size_t k = 0; k < pieces.size() && !stop(); ++k) {
+        if (!uploaded.wait(k)) break;
+        const Piece &p = pieces[k];
+        e = hipStreamWaitEvent(lane.enc, lane.ev_up[k], 0);
+        if (e == hipSuccess && k == 0) e = hipEventRecord(lane.t_enc0, lane.enc);
+        if (e != hipSuccess) break;
+        rc = gic_hip_encode_rows_src(a.fmt, a.src_type, p.d_slice, a.width, a.height, 1, a.channels, a.row_pitch,
+                                     p.y0, p.n, a.opt, p.d_out, nullptr, lane.enc);
+        if (rc != GIC_OK) break;
+        e = hipEventRecord(lane.ev_enc[k], lane.enc);
+        if (e != hipSuccess) break;
+        issued = k + 1;
+        encoded.post(issued);
+    }
+    if (issued && e == hipSuccess) e = hipEventRecord(lane.t_enc1, lane.enc);
+    encoded.fail();
+    if (rc != GIC_OK || e != hipSuccess) halt.store(true);   // the uploader stops at its next piece
+    uploader.join();
+    downloader.join();
+    const hipError_t es = hipStreamSynchronize(lane.enc);
+    if (e == hipSuccess) e = es;
+    const hipError_t eu = hipStreamSynchronize(lane.up);
+    if (e_up == hipSuccess) e_up = eu;
+    if (rc != GIC_OK) return rc;
+    if (e != hipSuccess || e_up != hipSuccess || e_dn != hipSuccess) return GIC_EHIP;
+    if (times && issued == pieces.size()) {
+        times->h2d_ms = span_ms(lane.t_up0, lane.t_up1);
+        times->encode_ms = span_ms(lane.t_enc0, lane.t_enc1);
+        bool any_dn = false;
+        for (const Piece &p : pieces) any_dn = any_dn || p.h_out;
+        times->d2h_ms = any_dn ? span_ms(lane.t_dn0, lane.t_dn1) : 0.0;
+    }
+    return GIC_OK;
+}
+
+}  // namespace gic

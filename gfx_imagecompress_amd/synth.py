@@ -64,6 +64,35 @@ def g1_torch(width: int, height: int, slices: int = 1, seed: int = 0x9E3779B9, d
     return out
 
 
+def g2(width: int, height: int, seed: int = 0x9E3779B9) -> np.ndarray:
+    """G0 plus independent noise per channel: n_c in [-8, 8] for R, G, B from
+    three hashes of the pixel index.  G1's single n moves a texel along the grey
+    axis, so its blocks stay nearly collinear; G2's noise is isotropic in RGB,
+    a harder case for BC7's line fits (the bounded exit's second content)."""
+    img = g0(width, height).astype(np.int64)
+    idx = np.arange(width * height, dtype=np.uint64).reshape(height, width)
+    for c in range(3):
+        key = np.uint64((seed + 0x632BE5AB * (c + 1)) & _M32)
+        img[..., c] += (_mix32(idx ^ key).astype(np.int64) % 17) - 8
+    return np.clip(img, 0, 255).astype(np.uint8)
+
+
+def g2_torch(width: int, height: int, seed: int = 0x9E3779B9, device="cuda"):
+    """Device-side G2 (bit-identical to :func:`g2`), shape (1, H, W, 4)."""
+    import torch
+    y = torch.arange(height, device=device, dtype=torch.int64).view(height, 1)
+    x = torch.arange(width, device=device, dtype=torch.int64).view(1, width)
+    base = (x * 255 // max(width - 1, 1), y * 255 // max(height - 1, 1),
+            (x + y) * 255 // max(width + height - 2, 1))
+    idx = y * width + x
+    out = torch.empty((1, height, width, 4), dtype=torch.uint8, device=device)
+    for c in range(3):
+        n = (_mix32(idx ^ ((seed + 0x632BE5AB * (c + 1)) & _M32)) % 17) - 8
+        out[0, ..., c] = (base[c] + n).clamp(0, 255).to(torch.uint8)
+    out[0, ..., 3] = 255
+    return out
+
+
 def noise_rgba(width: int, height: int, seed: int = 1, alpha: bool = False) -> np.ndarray:
     rng = np.random.default_rng(seed)
     img = rng.integers(0, 256, size=(height, width, 4), dtype=np.uint8)

@@ -15,6 +15,7 @@
 #ifndef GFX_IMAGECOMPRESS_AMD_GIC_H_
 #define GFX_IMAGECOMPRESS_AMD_GIC_H_
 
+#include <stdbool.h>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -26,6 +27,7 @@ extern "C" {
 #define GIC_EINVAL (-1)
 #define GIC_EUNSUP (-2)
 #define GIC_EHIP (-3)
+#define GIC_EABORT (-4)   /* a progress callback asked to stop */
 
 typedef enum gic_format {
     GIC_FMT_BC1 = 1, /* Image_CompressAMDBC1Block semantics (amd_bcx_helpers.cpp:51) */
@@ -143,8 +145,10 @@ int gic_hip_encode_rows_src(gic_format fmt, gic_source src_type, const void *d_s
 typedef struct gic_multi_report {
     int ranks;               /* devices in the list */
     int rccl;                /* 1: the gather ran over RCCL, 0: peer copies */
-    double encode_ms_max;    /* the slowest device's upload + encode (HIP events on its stream) */
-    double gather_ms;        /* the gather on the root's stream */
+    double encode_ms_max;    /* call start -> the slowest device's last encoded piece (host clock;
+                                uploads and encodes pipelined per device) */
+    double gather_ms;        /* the gather's exposed part: that moment -> the call's end (each
+                                device sends as soon as its own encode is done) */
     uint64_t gathered_bytes; /* packed bytes received from the other devices */
 } gic_multi_report;
 int gic_encode_multi(gic_format fmt, gic_source src_type, const void *h_src, uint32_t width, uint32_t height,
@@ -156,6 +160,40 @@ int gic_multi_last_report(gic_multi_report *out);
 int gic_multi_release(void);
 /* the split: device i's first slice-major block row and row count (host only) */
 int gic_multi_split(uint64_t rows_total, int ndev, int i, uint64_t *first, uint64_t *rows);
+
+/* Host images (the Image_Compress* entry points and gic_compress_image).  The
+ * reference's wrappers take a host image and return one (amd_bc1_compressor.cpp:
+ * 36-70); here the block rows are cut into pieces (about 2^18 blocks, BC7 2^20)
+ * and each device pipelines them: the upload of piece k+1 and the download of
+ * piece k-1 overlap the encode of piece k (gic_pipeline.cpp).  The upload mode
+ * is the environment variable GIC_H2D: "pageable" (default: hipMemcpyAsync from
+ * the caller's memory), "staged" (through a pinned ring) or "register"
+ * (hipHostRegister of the caller's range for the call).  With GIC_DEVICES
+ * listing several devices, every device pipelines its contiguous share of the
+ * rows and downloads its blocks straight into the host image (no device
+ * gather); a progress callback sees the reference's per-row sequence in the
+ * reference's order in both cases, and returning true aborts (NULL). */
+typedef struct gic_host_report {
+    int devices;       /* devices the call ran on */
+    int pieces;        /* pieces of block rows, over all devices */
+    int h2d_mode;      /* 0 pageable, 1 staged, 2 register */
+    double total_ms;   /* the whole call, host clock */
+    double h2d_ms;     /* first upload start -> last upload end (HIP events; the slowest device) */
+    double encode_ms;  /* first encode start -> last encode end */
+    double d2h_ms;     /* first download start -> last download end */
+} gic_host_report;
+/* the calling thread's last host-image call */
+int gic_last_host_report(gic_host_report *out);
+/* Any format on a host image with explicit options (the Image_Compress*
+ * wrappers fix the options the reference fixes; this entry takes them all, e.g.
+ * the BC7 search options bc7_mse_bound / bc7_shake_ranks).  Destination format:
+ * the wrappers' choice for the format (BC1: the RGBA variant for 4-channel
+ * sources), sRGB for sRGB sources, SNORM BC4/BC5 for signed ones, BC6H signed for
+ * GIC_FMT_BC6H_SF.  NULL on failure or abort; free with Image_Destroy. */
+struct Image_ImageHeader;
+struct Image_ImageHeader const *gic_compress_image(struct Image_ImageHeader const *src, gic_format fmt,
+                                                   const gic_options *opt, bool (*progress)(void *user, float pct),
+                                                   void *user);
 
 /* Block-level batch: n blocks of 16 texels, float in [0,1].
  *   BC1/BC2/BC3/BC7: d_blocks holds n x 64 floats (RGBA per texel, texel-major).
@@ -248,6 +286,13 @@ int gic_iter_cap_hits(unsigned long long *hits, int reset);
 int gic_set_iter_cap(int cap);
 int gic_nonterminating_loops(unsigned long long *loops, int reset);
 int gic_last_h4_report(uint32_t *rerun_blocks, uint32_t *nonterminating_loops);
+
+/* Stages of the calling thread's last BC7 device call: *stages = 4 with the
+ * bounded exit (bc7_mse_bound > 0: the mode-6, mode-3 and mode-1 probes, then
+ * the full search; fewer if the mode mask drops a probe), 1 without; blocks_in[k]
+ * = blocks entering stage k (0 once no block is left).  The bounded exit's
+ * probe-exit share is 1 - blocks_in[stages - 1] / blocks_in[0]. */
+int gic_last_bc7_stages(uint32_t blocks_in[4], int *stages);
 
 /* Library version string. */
 const char *gic_version(void);

@@ -123,3 +123,85 @@ def test_multi_rejects_bad_arguments(gpu):
         gic.encode_multi(gic.FMT_BC1, img, [99], dst)
     with pytest.raises(gic.GicError):
         gic.encode_multi(gic.FMT_BC1, img, [], dst)
+
+
+# ---------------------------------------------------------------------------
+# the host-image pipeline (gic_pipeline.cpp): upload / encode / download overlap
+
+
+def _progress_run(fmt, img, entry=None, abort_at=None, options=None):
+    seen = []
+
+    def cb(pct):
+        seen.append(pct)
+        return abort_at is not None and pct > abort_at
+    out = gic.compress_host(fmt, img, options, progress=cb, entry=entry)
+    return out, seen
+
+
+@pytest.mark.parametrize("mode", ["pageable", "staged", "register"])
+def test_host_pipeline_modes_and_pieces(gpu, monkeypatch, mode):
+    """Every upload mode, cut into many pieces (GIC_PIECE_BLOCKS), over three
+    slices whose pieces end inside and at slice ends: the same bytes as the
+    device path, and the report counts the pieces."""
+    img = np.stack([synth.noise_rgba(203, 141, seed=11 + k) for k in range(3)])
+    ref = gpu_encode(gic.FMT_BC1, img).reshape(3, 36, 51, 8)
+    monkeypatch.setenv("GIC_H2D", mode)
+    monkeypatch.setenv("GIC_PIECE_BLOCKS", str(51 * 5))   # 5 block rows a piece: 8 per slice
+    got = gic.compress_host(gic.FMT_BC1, img, gic.Options())
+    assert np.array_equal(got, ref)
+    rep = gic.host_report()
+    assert rep["devices"] == 1 and rep["pieces"] == 3 * 8
+    assert rep["h2d_mode"] == ["pageable", "staged", "register"].index(mode)
+    assert rep["total_ms"] > 0 and rep["h2d_ms"] > 0 and rep["encode_ms"] > 0 and rep["d2h_ms"] > 0
+
+
+def test_host_pipeline_progress_sequence_single_and_multi(gpu, monkeypatch):
+    """Image_CompressAMDBC1 with a progress callback: one device, and
+    GIC_DEVICES=0,0,0 (three lanes, every lane downloading its rows straight
+    into the host image) -- the same bytes and exactly the reference's per-row
+    sequence 100 * (y * bx) / (bx * by), slice by slice, in order
+    (amd_bc1_compressor.cpp:64-68); a callback returning true gives NULL."""
+    img = np.stack([synth.noise_rgba(96, 42, seed=21 + k) for k in range(2)])
+    bx, by = 24, 11
+    want = [np.float32(100.0) * np.float32(y * bx) / np.float32(bx * by) for _ in range(2) for y in range(by)]
+    monkeypatch.setenv("GIC_PIECE_BLOCKS", str(bx * 2))
+    ref, seq = _progress_run(gic.FMT_BC1, img, entry="Image_CompressAMDBC1")
+    assert ref is not None and np.array_equal(ref, gpu_encode(gic.FMT_BC1, img).reshape(2, by, bx, 8))
+    assert np.array_equal(np.array(seq, np.float32), np.array(want, np.float32))
+    for devs in ("0,0,0", "0,0,0,0,0"):
+        monkeypatch.setenv("GIC_DEVICES", devs)
+        got, seq = _progress_run(gic.FMT_BC1, img, entry="Image_CompressAMDBC1")
+        assert np.array_equal(got, ref), devs
+        assert np.array_equal(np.array(seq, np.float32), np.array(want, np.float32)), devs
+        assert gic.host_report()["devices"] == len(devs.split(","))
+        out, seq = _progress_run(gic.FMT_BC1, img, entry="Image_CompressAMDBC1", abort_at=50.0)
+        assert out is None and seq[-1] > 50.0 and len(seq) < len(want)
+    # BC7 through its wrapper over three lanes
+    small = np.ascontiguousarray(synth.g1(32, 12))
+    monkeypatch.setenv("GIC_DEVICES", "0,0,0")
+    got7, seq7 = _progress_run(gic.FMT_BC7, small, entry="Image_CompressAMDBC7")
+    assert np.array_equal(got7.reshape(-1, 16), gpu_encode(gic.FMT_BC7, small))
+    assert len(seq7) == 3
+    assert gic.library().gic_multi_release() == 0
+
+
+def test_compress_image_options(gpu):
+    """gic_compress_image takes every option: the BC7 bounded exit through the
+    host path equals the device path's blocks with the same options."""
+    img = np.ascontiguousarray(synth.g1(64, 32))
+    o = gic.Options(bc7_mse_bound=0.5)
+    got = gic.compress_host(gic.FMT_BC7, img, o)
+    assert np.array_equal(got.reshape(-1, 16), gpu_encode(gic.FMT_BC7, img, o))
+    got5 = gic.compress_host(gic.FMT_BC5, np.ascontiguousarray(img[..., :2]), gic.Options())
+    assert np.array_equal(got5.reshape(-1, 16), gpu_encode(gic.FMT_BC5, np.ascontiguousarray(img[..., :2])))
+
+
+def test_encode_multi_checks_dst_device_and_dtype(gpu):
+    import torch
+    img = synth.g1(16, 16)
+    dst = torch.zeros(16 * 8, dtype=torch.uint8, device="cuda")
+    with pytest.raises(gic.GicError):
+        gic.encode_multi(gic.FMT_BC1, img.astype(np.float32), [0], dst)   # float data, UNORM8 source type
+    with pytest.raises(gic.GicError):
+        gic.encode_multi(gic.FMT_BC1, img, [0], torch.zeros(16 * 8, dtype=torch.uint8))   # host dst
