@@ -1059,9 +1059,12 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
     mean_of(data, mean, n, dim);
 #ifdef ORC_STATS
     unsigned long long psig[512];
-    int npsig = 0, st_dup_ = 0;
+    int npsig = 0, st_dup_ = 0, st_round_ = -1;
 #endif
     do {
+#ifdef ORC_STATS
+        if (++st_round_ > 0) ST(55, 1);
+#endif
         collapse(index, n);
         const int Mi = max_index(index, n);
         int p0 = -1, q0 = -1, idx2[16] = {0}, epo2[2][4] = {{0}};
@@ -1202,6 +1205,33 @@ static double shake_corners(double data[][4], int n, int *index_, int epo_code[2
                                     mn = e < mn ? e : mn;
                                 }
                                 if (!st_dup_) { ST(38, 1); ST(39, mn < thr_); ST(40, mn < err1_in_); }
+                                if (!st_dup_) { /* per-channel separable lower bounds of every corner's error */
+                                    double lb_all = 0, lb_2 = 0;
+                                    for (int j = 0; j < dim; ++j) {
+                                        double ba = DBL_MAX, b2 = DBL_MAX;
+                                        for (int cb = 0; cb < 4; ++cb) {
+                                            double sa = 0, s2 = 0;
+                                            for (int i = 0; i < n; ++i) {
+                                                double bm = DBL_MAX;
+                                                for (int c = 0; c < nc; ++c) {
+                                                    const double rv = shake_ramp(clog, bits[j], epi[0][j][cb & 1], epi[1][j][cb >> 1], c);
+                                                    const double d = (rv - data[i][j]) * (rv - data[i][j]);
+                                                    bm = d < bm ? d : bm;
+                                                }
+                                                sa += bm;
+                                                if (i < 2) s2 += bm;
+                                            }
+                                            ba = sa < ba ? sa : ba;
+                                            b2 = s2 < b2 ? s2 : b2;
+                                        }
+                                        lb_all += ba;
+                                        lb_2 += b2;
+                                    }
+                                    ST(52, lb_all >= thr_);
+                                    ST(53, mn >= thr_);
+                                    ST(54, lb_2 >= thr_);
+                                    ST(57 + (st_round_ > 0), 1);
+                                }
                             }
                             if (!st_dup_) { /* walked passes: texels under the natural, distance and min-contribution orders */
                                 int ord3[16];

@@ -16,8 +16,9 @@ mkdir -p "$O"
 cd "$R" || exit 1
 case "$STEP" in
 tests)
-  K=${1:+-k "$1"}
-  timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread $K \
+  K=()
+  [ -n "$1" ] && K=(-k "$1")
+  timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" \
     > "$O/gpu_tests.log" 2>&1 || { tail -40 "$O/gpu_tests.log"; exit 1; }
   tail -3 "$O/gpu_tests.log"
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" >> "$O/gpu_tests.log" 2>&1 \
