@@ -16,6 +16,8 @@
 // 512*510^2 + 103*803^2 + 18*946^2 + 128*255^2 < 2.3e8) times 16 texels stays
 // below 2^32, so the reference's uint64 totals never exceed 32 bits and
 // 0xffffffff can stand for its UINT64_MAX "no solution yet".
+#include <type_traits>
+
 #include "bc7_tables.h"
 #include "bc7enc_tables.h"
 #include "gic_common.h"
@@ -44,15 +46,6 @@ __device__ __forceinline__ float sat(float v) { return clampf_r(v, 0.f, 1.0f); }
 __device__ __forceinline__ int clampi_r(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 __device__ __forceinline__ uint32_t sel_at(uint64_t s, int i) { return (uint32_t)(s >> (4 * i)) & 15u; }
 
-// A texel word the optimiser must treat as new at every use: without it the
-// per-texel channel values and their float conversions (16 x 4 each) are hoisted
-// out of the trial loops and held live, which spills the kernel.
-__device__ __forceinline__ uint32_t tex(const uint32_t px[16], int i)
-{
-    uint32_t v = px[i];
-    asm volatile("" : "+v"(v));
-    return v;
-}
 
 // g_bc7_weights3/4 (:130-131): round(64 s / (N - 1))
 __device__ __forceinline__ uint32_t bc7w(uint32_t s, uint32_t N)
@@ -88,17 +81,34 @@ struct Res {            // color_cell_compressor_results :297-305
     uint64_t sel;       // selector of texel i in nibble i (texels of the subset only)
 };
 
-// per-texel transforms of the perceptual metric, computed once per block and
-// parked in the workgroup's LDS (rows l 0..15, cr 16..31, cb 32..47, each row
-// 256 lanes wide, so a wave's reads are conflict-free).  Held in registers
-// they were 48 VGPRs live through the whole search (2 waves per SIMD); the
-// read address is opaque at every use so the loads stay inside the ramp loops.
-// (STRIDE = the workgroup's lanes: 256 for the lane-per-block kernels, 64 for
-// the one-wave block kernel, whose 48 rows then take 12 KB instead of 48 KB)
-constexpr uint32_t kYccStride = 256;
+// The block's texels live in the workgroup's LDS, not in registers: with the
+// 16 texel words held through the whole search the lane kernels spilled ~100
+// VGPRs at 3 waves/SIMD (8x the algorithmic HBM bytes in scratch traffic,
+// round 5).  Each lane owns a column of rows (row r of lane t at word r *
+// STRIDE + t, so a wave's reads are conflict-free; STRIDE = the workgroup's
+// lanes: 256 for the lane-per-block kernels, 64 for the one-wave block
+// kernel).  The read address is opaque at every use, so the loads stay where
+// the texels are used instead of being hoisted back into registers.
+//
+// Perceptual metric (YccT): rows 0..15 / 16..31 / 32..47 hold the texel's
+// transforms l, cr, cb (compute_color_distance_rgb, :331-339) scaled by 2^13,
+// less one unit of 2^13, with the texel's bytes in the low bits:
+//   L  = (l  - 1) * 2^13 + (1 | r << 1 | (a & 15) << 9)
+//   CR = (cr - 1) * 2^13 + (1 | g << 1 | (a >> 4) << 9)
+//   CB = (cb - 1) * 2^13 + (1 | b << 1)
+// (low parts in [1, 8191]).  A ramp colour's transforms are scaled by 2^13
+// exactly (ycc_ramp: the same three multiply-adds with scaled constants), so
+// for a ramp point and a texel L1 - L2 = (l1 - l2) * 2^13 + d with d in
+// [1, 8191]: d never carries past a multiple of 2^21, and (L1 - L2) >> 21 =
+// (l1 - l2) >> 8 exactly, likewise CR and CB; every difference stays inside
+// int32 (|cr1 - cr2| <= 261120, * 2^13 + 8191 < 2^31).  So the metric costs
+// what it did with plain l / cr / cb rows, and the texel words need no rows of
+// their own (48 rows, 48 KB per workgroup: the LDS budget of 3 workgroups per
+// CU); a texel's bytes come back with one bit-field extract each.
 template <uint32_t STRIDE>
 struct YccT {
     uint32_t a;   // LDS byte address of this lane's row-0 word
+    static constexpr uint32_t kRows = 48;
     __device__ __forceinline__ int at(int row) const
     {
         uint32_t b = a;
@@ -108,15 +118,70 @@ struct YccT {
     __device__ __forceinline__ int l(int i) const { return at(i); }
     __device__ __forceinline__ int cr(int i) const { return at(16 + i); }
     __device__ __forceinline__ int cb(int i) const { return at(32 + i); }
-    __device__ __forceinline__ void put(int i, int l_, int cr_, int cb_) const
+    __device__ __forceinline__ uint32_t word(int i) const
+    {
+        const uint32_t x = (uint32_t)l(i), y = (uint32_t)cr(i), z = (uint32_t)cb(i);
+        return __builtin_amdgcn_ubfe(x, 1, 8) | __builtin_amdgcn_ubfe(y, 1, 8) << 8 | __builtin_amdgcn_ubfe(z, 1, 8) << 16 |
+               __builtin_amdgcn_ubfe(x, 9, 4) << 24 | __builtin_amdgcn_ubfe(y, 9, 4) << 28;
+    }
+    // texel i's channels (alpha only when asked for, else 0)
+    __device__ __forceinline__ void chans(int i, bool alpha, uint32_t c[4]) const
+    {
+        const uint32_t x = (uint32_t)l(i), y = (uint32_t)cr(i), z = (uint32_t)cb(i);
+        c[0] = __builtin_amdgcn_ubfe(x, 1, 8);
+        c[1] = __builtin_amdgcn_ubfe(y, 1, 8);
+        c[2] = __builtin_amdgcn_ubfe(z, 1, 8);
+        c[3] = alpha ? __builtin_amdgcn_ubfe(x, 9, 4) | __builtin_amdgcn_ubfe(y, 9, 4) << 4 : 0u;
+    }
+    __device__ __forceinline__ void put(int i, uint32_t w) const
     {
         typedef __attribute__((address_space(3))) int lds_i32;
-        *(lds_i32 *)(size_t)(a + 4u * (uint32_t)i * STRIDE) = l_;
-        *(lds_i32 *)(size_t)(a + 4u * (uint32_t)(16 + i) * STRIDE) = cr_;
-        *(lds_i32 *)(size_t)(a + 4u * (uint32_t)(32 + i) * STRIDE) = cb_;
+        const int r = (int)(w & 0xffu), g = (int)((w >> 8) & 0xffu), b = (int)((w >> 16) & 0xffu);
+        const int al = (int)(w >> 24);
+        const int l_ = r * 109 + g * 366 + b * 37;
+        const int cr_ = (r << 9) - l_, cb_ = (b << 9) - l_;
+        *(lds_i32 *)(size_t)(a + 4u * (uint32_t)i * STRIDE) = (l_ - 1) * 8192 + (1 | r << 1 | (al & 15) << 9);
+        *(lds_i32 *)(size_t)(a + 4u * (uint32_t)(16 + i) * STRIDE) = (cr_ - 1) * 8192 + (1 | g << 1 | (al >> 4) << 9);
+        *(lds_i32 *)(size_t)(a + 4u * (uint32_t)(32 + i) * STRIDE) = (cb_ - 1) * 8192 + (1 | b << 1);
     }
 };
+template <uint32_t STRIDE>
+struct TexT {
+    uint32_t a;
+    static constexpr uint32_t kRows = 16;
+    __device__ __forceinline__ int at(int row) const
+    {
+        uint32_t b = a;
+        asm volatile("" : "+v"(b));
+        return *(const __attribute__((address_space(3))) int *)(size_t)(b + 4u * (uint32_t)row * STRIDE);
+    }
+    __device__ __forceinline__ int l(int) const { return 0; }   // (perceptual paths only)
+    __device__ __forceinline__ int cr(int) const { return 0; }
+    __device__ __forceinline__ int cb(int) const { return 0; }
+    __device__ __forceinline__ uint32_t word(int i) const { return (uint32_t)at(i); }
+    __device__ __forceinline__ void chans(int i, bool alpha, uint32_t c[4]) const
+    {
+        const uint32_t w = word(i);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) c[k] = ch(w, k);
+        c[3] = alpha ? ch(w, 3) : 0u;
+    }
+    __device__ __forceinline__ void put(int i, uint32_t w) const
+    {
+        *(__attribute__((address_space(3))) int *)(size_t)(a + 4u * (uint32_t)i * STRIDE) = (int)w;
+    }
+};
+constexpr uint32_t kYccStride = 256;
 using Ycc = YccT<kYccStride>;
+template <bool P, uint32_t STRIDE>
+using TexSrc = typename std::conditional<P, YccT<STRIDE>, TexT<STRIDE>>::type;
+
+// a texel word of the block (from LDS, see above)
+template <class Y>
+__device__ __forceinline__ uint32_t tex(const Y &y, int i)
+{
+    return y.word(i);
+}
 
 // scale_color :307-323 (n = component bits + p-bit)
 __device__ __forceinline__ uint32_t expand(uint32_t q, uint32_t n)
@@ -130,12 +195,13 @@ __device__ __forceinline__ uint32_t expand(uint32_t q, uint32_t n)
     return r;
 }
 
-// the YCbCr-style transform of compute_color_distance_rgb (:331-339)
-__device__ __forceinline__ void ycc(int r, int g, int b, int &l, int &cr, int &cb)
+// the YCbCr-style transform of compute_color_distance_rgb (:331-339) of a
+// ramp colour, scaled by 2^13 (see YccT)
+__device__ __forceinline__ void ycc_ramp(int r, int g, int b, int &l, int &cr, int &cb)
 {
-    l = r * 109 + g * 366 + b * 37;
-    cr = (r << 9) - l;
-    cb = (b << 9) - l;
+    l = r * (109 * 8192) + g * (366 * 8192) + b * (37 * 8192);
+    cr = (r << 22) - l;
+    cb = (b << 22) - l;
 }
 
 // weighted squared distance w0 d0^2 + w1 d1^2 + w2 d2^2 [+ e]
@@ -153,11 +219,12 @@ __device__ __forceinline__ uint32_t wsq(int d0, int d1, int d2, const EncCfg &cf
     return (uint32_t)e + __umul24(cf.w[0], s0) + __umul24(cf.w[1], s1) + __umul24(cf.w[2], s2);
 }
 
-// compute_color_distance_rgb with perceptual = true, from the two colours' transforms
+// compute_color_distance_rgb with perceptual = true, from a ramp colour's
+// packed transforms (ycc_ramp) and a texel's (YccT): (l1 - l2) >> 8 etc.
 __device__ __forceinline__ uint32_t ycc_err(int l1, int cr1, int cb1, int l2, int cr2, int cb2, const EncCfg &cf,
                                             int e = 0)
 {
-    return wsq((l1 - l2) >> 8, (cr1 - cr2) >> 8, (cb1 - cb2) >> 8, cf, e);
+    return wsq((l1 - l2) >> 21, (cr1 - cr2) >> 21, (cb1 - cb2) >> 21, cf, e);
 }
 
 // The search below runs K subset problems in lockstep: K = 1 is one problem on
@@ -204,7 +271,7 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
 template <bool P, int K, class Y = Ycc, bool WAVE = false>
 __device__ __forceinline__ void evaluate(const uint32_t lo[K], const uint32_t hi[K], const uint32_t pb0[K],
                                          const uint32_t pb1[K], const bool want[K], const Prob pr[K], uint32_t m0,
-                                         const uint32_t px[16], const Y &tx, const EncCfg &cf, Res r[K])
+                                         const Y &px, const Y &tx, const EncCfg &cf, Res r[K])
 {
     uint32_t a[K], b[K];
 #pragma unroll
@@ -280,15 +347,13 @@ __device__ __forceinline__ void evaluate(const uint32_t lo[K], const uint32_t hi
         const int i = L & 15;
         const bool f0 = first_subset<K>(m0, i);
         const uint32_t A = f0 ? a[0] : a[K - 1], B = f0 ? b[0] : b[K - 1];
-        uint32_t c = px[0];
-#pragma unroll
-        for (int t = 1; t < 16; ++t) c = i == t ? px[t] : c;
+        const uint32_t c = tex(px, i);
         const int tl = tx.l(i), tcr = tx.cr(i), tcb = tx.cb(i);
         uint32_t key = kNone;
         for (uint32_t j = (uint32_t)(L >> 4); j < N; j += 4) {
             const uint32_t w = bc7w(j, N);
             int l1, cr1, cb1;
-            ycc(lerp_ch(A, B, 0, w), lerp_ch(A, B, 1, w), lerp_ch(A, B, 2, w), l1, cr1, cb1);
+            ycc_ramp(lerp_ch(A, B, 0, w), lerp_ch(A, B, 1, w), lerp_ch(A, B, 2, w), l1, cr1, cb1);
             int ea = 0;
             if (any_alpha) {   // wave-uniform; K == 1
                 const int d = lerp_ch(A, B, 3, w) - (int)ch(c, 3);
@@ -317,8 +382,8 @@ __device__ __forceinline__ void evaluate(const uint32_t lo[K], const uint32_t hi
             int l1[K], cr1[K], cb1[K];
 #pragma unroll
             for (int s = 0; s < K; ++s)
-                ycc(lerp_ch(a[s], b[s], 0, w), lerp_ch(a[s], b[s], 1, w), lerp_ch(a[s], b[s], 2, w), l1[s], cr1[s],
-                    cb1[s]);
+                ycc_ramp(lerp_ch(a[s], b[s], 0, w), lerp_ch(a[s], b[s], 1, w), lerp_ch(a[s], b[s], 2, w), l1[s],
+                         cr1[s], cb1[s]);
             if (any_alpha) {   // wave-uniform; K == 1
                 const int a1 = lerp_ch(a[0], b[0], 3, w);
 #pragma unroll
@@ -442,7 +507,7 @@ __device__ __forceinline__ void quantize(float xl[4], float xh[4], const Prob &p
 // endpoints, evaluate those that differ from its best (:710, :724)
 template <bool P, int K, class Y = Ycc, bool WAVE = false>
 __device__ __forceinline__ void fit(float xl[K][4], float xh[K][4], const bool active[K], const Prob pr[K],
-                                    uint32_t m0, const uint32_t px[16], const Y &tx, const EncCfg &cf, Res r[K])
+                                    uint32_t m0, const Y &px, const Y &tx, const EncCfg &cf, Res r[K])
 {
     uint32_t lo[K], hi[K], p0[K], p1[K];
     bool want[K], any = false;
@@ -459,11 +524,12 @@ __device__ __forceinline__ void fit(float xl[K][4], float xh[K][4], const bool a
 // compute_least_squares_endpoints_rgb / _rgba :197-280 for the K problems in
 // one texel pass (each texel adds to its own subset's sums, in texel order),
 // then the 1/255 scale
-template <int K>
-__device__ __forceinline__ void lsq(const Prob pr[K], uint32_t m0, uint64_t sel, const uint32_t px[16],
+template <int K, class Y>
+__device__ __forceinline__ void lsq(const Prob pr[K], uint32_t m0, uint64_t sel, const Y &px,
                                     const EncLds &L, float xl[K][4], float xh[K][4])
 {
     const float *wx = L.wx + (pr[0].nsel == 16 ? 32 : 0);
+    const bool need_a = K == 1 && __any(pr[0].alpha);   // wave-uniform; mode-1 problems are opaque
     float z00[K], z10[K], z11[K], q00[K][4], t[K][4];
 #pragma unroll
     for (int s = 0; s < K; ++s) {
@@ -477,7 +543,8 @@ __device__ __forceinline__ void lsq(const Prob pr[K], uint32_t m0, uint64_t sel,
         const bool in = K == 2 || ((pr[0].mask >> i) & 1u);
         const float *w4 = wx + 4 * sel_at(sel, i);
         const float w = w4[3];
-        const uint32_t c = tex(px, i);
+        uint32_t c[4];
+        px.chans(i, need_a, c);
 #pragma unroll
         for (int s = 0; s < K; ++s) {
             const bool add = in && (s == 0 ? f0 : !f0);
@@ -486,7 +553,8 @@ __device__ __forceinline__ void lsq(const Prob pr[K], uint32_t m0, uint64_t sel,
             z11[s] = add ? z11[s] + w4[2] : z11[s];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const float v = (float)ch(c, k);
+                if (k == 3 && !need_a) break;   // (alpha sums are only read by alpha problems)
+                const float v = (float)c[k];
                 q00[s][k] = add ? q00[s][k] + w * v : q00[s][k];
                 t[s][k] = add ? t[s][k] + v : t[s][k];
             }
@@ -511,7 +579,7 @@ __device__ __forceinline__ void lsq(const Prob pr[K], uint32_t m0, uint64_t sel,
 
 // pack_mode1_to_one_color :357-403
 template <bool P, class Y = Ycc>
-__device__ __forceinline__ void one_colour(uint32_t cr, uint32_t cg, uint32_t cb, const Prob &pr, const uint32_t px[16], const Y &tx,
+__device__ __forceinline__ void one_colour(uint32_t cr, uint32_t cg, uint32_t cb, const Prob &pr, const Y &px, const Y &tx,
                            const EncCfg &cf, const EncLds &L, Res &r)
 {
     uint32_t best = kNone, bp = 0;
@@ -535,7 +603,7 @@ __device__ __forceinline__ void one_colour(uint32_t cr, uint32_t cg, uint32_t cb
         q[k] = (int)((lo * (64u - 18u) + hi * 18u + 32u) >> 6);
     }
     int ql, qcr, qcb;
-    ycc(q[0], q[1], q[2], ql, qcr, qcb);
+    ycc_ramp(q[0], q[1], q[2], ql, qcr, qcb);
     uint32_t tot = 0;
     uint64_t ts = 0;
 #pragma unroll
@@ -551,20 +619,39 @@ __device__ __forceinline__ void one_colour(uint32_t cr, uint32_t cg, uint32_t cb
     r.err = tot;
 }
 
-// color_cell_compression :756-874: the subset's mean and principal axis, and the
-// PCA endpoints the first fit starts from
-template <bool P>
-__device__ __forceinline__ void pca_endpoints(const Prob &pr, const uint32_t px[16], float cmin[4], float cmax[4],
-                                              float mn[4])
+// the subset's channel sums in texel order (exact: integers below 2^24)
+template <class Y>
+__device__ __forceinline__ void subset_sums(const Prob &pr, const Y &px, float m[4])
 {
-    // mean and principal axis (:756-841)
-    float m[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) m[k] = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const bool in = (pr.mask >> i) & 1u;
 #pragma unroll
         for (int k = 0; k < 4; ++k) m[k] = in ? m[k] + (float)ch(tex(px, i), k) : m[k];
     }
+}
+
+// the subset mean as color_cell_compression scales it (:766-771)
+template <class Y>
+__device__ __forceinline__ void subset_mean(const Prob &pr, const Y &px, float mn[4])
+{
+    float m[4];
+    subset_sums(pr, px, m);
+    const float inv_n255 = 1.0f / (float)(pr.n * 255.0f);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) mn[k] = sat(m[k] * inv_n255);
+}
+
+// color_cell_compression :756-874: the subset's mean and principal axis, and the
+// PCA endpoints the first fit starts from
+template <bool P, class Y>
+__device__ __forceinline__ void pca_endpoints(const Prob &pr, const Y &px, float cmin[4], float cmax[4])
+{
+    // mean and principal axis (:756-841)
+    float m[4], mn[4];
+    subset_sums(pr, px, m);
     float ms[4], ax[4] = {0.f, 0.f, 0.f, 0.f};
     const float inv_n = 1.0f / (float)pr.n, inv_n255 = 1.0f / (float)(pr.n * 255.0f);
 #pragma unroll
@@ -671,11 +758,10 @@ __device__ __forceinline__ void pca_endpoints(const Prob &pr, const uint32_t px[
 
 // color_cell_compression :731-1024 for K problems in lockstep
 template <bool P, int K, class Y = Ycc, bool WAVE = false>
-__device__ __forceinline__ void cells(const Prob pr[K], uint32_t m0, const uint32_t px[16], const Y &tx,
+__device__ __forceinline__ void cells(const Prob pr[K], uint32_t m0, const Y &px, const Y &tx,
                                       const EncCfg &cf, const EncLds &L, Res r[K])
 {
     bool fin[K];   // the subset was packed as one colour (:738-754): no trials
-    float cmin[K][4], cmax[K][4], mn[K][4];
 #pragma unroll
     for (int s = 0; s < K; ++s) {
         r[s].err = kNone;
@@ -695,7 +781,6 @@ __device__ __forceinline__ void cells(const Prob pr[K], uint32_t m0, const uint3
                 fin[s] = true;
             }
         }
-        if (!fin[s]) pca_endpoints<P>(pr[s], px, cmin[s], cmax[s], mn[s]);
     }
 
     // Trials, each a fit that keeps the best (:874-1006): t = 0 the PCA endpoints;
@@ -741,10 +826,14 @@ __device__ __forceinline__ void cells(const Prob pr[K], uint32_t m0, const uint3
         if (!any) break;   // color_cell_compression returned (0) or finished its trials
         float xl[K][4], xh[K][4];
         if (t == 0) {
+            // the PCA endpoints, computed here so that nothing of them stays live
+            // through the trials (register budget)
 #pragma unroll
-            for (int s = 0; s < K; ++s)
+            for (int s = 0; s < K; ++s) {
 #pragma unroll
-                for (int k = 0; k < 4; ++k) xl[s][k] = cmin[s][k], xh[s][k] = cmax[s][k];
+                for (int k = 0; k < 4; ++k) xl[s][k] = xh[s][k] = 0.f;
+                if (active[s]) pca_endpoints<P, Y>(pr[s], px, xl[s], xh[s]);
+            }
         } else {
             uint64_t ts = 0;
             if (t <= nls) {
@@ -775,7 +864,7 @@ __device__ __forceinline__ void cells(const Prob pr[K], uint32_t m0, const uint3
                     ts |= (uint64_t)(uint32_t)clampf_r(v, 0, (float)maxs) << (4 * i);
                 }
             }
-            lsq<K>(pr, m0, ts, px, L, xl, xh);
+            lsq<K, Y>(pr, m0, ts, px, L, xl, xh);
         }
         fit<P, K, Y, WAVE>(xl, xh, active, pr, m0, px, tx, cf, r);
 #pragma unroll
@@ -785,8 +874,10 @@ __device__ __forceinline__ void cells(const Prob pr[K], uint32_t m0, const uint3
     for (int s = 0; s < K; ++s) {
         if (pr[s].mode1 && !fin[s] && !zero[s]) {   // the subset mean as one colour (:1009-1021)
             Res avg = r[s];
-            one_colour<P>((uint32_t)(int)(.5f + mn[s][0] * 255.0f), (uint32_t)(int)(.5f + mn[s][1] * 255.0f),
-                          (uint32_t)(int)(.5f + mn[s][2] * 255.0f), pr[s], px, tx, cf, L, avg);
+            float mn[4];
+            subset_mean(pr[s], px, mn);   // recomputed: the same sums as pca_endpoints'
+            one_colour<P>((uint32_t)(int)(.5f + mn[0] * 255.0f), (uint32_t)(int)(.5f + mn[1] * 255.0f),
+                          (uint32_t)(int)(.5f + mn[2] * 255.0f), pr[s], px, tx, cf, L, avg);
             if (avg.err < r[s].err) r[s] = avg;
         }
     }
@@ -823,8 +914,26 @@ __device__ __forceinline__ void est_setup(EstSubset &e)
 // are non-negative and the caller keeps a total only if it is strictly less),
 // so the sum stops -- the reference's own early exit (:1156-1157), taken per
 // wave after every two texels.
+// The block's texel words in registers, for the partition estimate's phase
+// (its shapes re-read every texel; nothing of the trials is live then).
+struct RegTex {
+    uint32_t w[16];
+    template <class Y>
+    __device__ __forceinline__ void load(const Y &y)
+    {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = y.word(i);
+    }
+    __device__ __forceinline__ uint32_t word(int i) const
+    {
+        uint32_t v = w[i];
+        asm volatile("" : "+v"(v));   // new at every use: keeps the channel conversions out of the shape loop
+        return v;
+    }
+};
+
 template <bool P, class Y = Ycc>
-__device__ __forceinline__ uint32_t estimate2(uint32_t m0, const uint32_t px[16], const Y &tx, const EncCfg &cf,
+__device__ __forceinline__ uint32_t estimate2(uint32_t m0, const RegTex &px, const Y &tx, const EncCfg &cf,
                                               uint32_t best)
 {
     EstSubset s0, s1;
@@ -869,7 +978,7 @@ __device__ __forceinline__ uint32_t estimate2(uint32_t m0, const uint32_t px[16]
         for (int k = 0; k < 3; ++k) c[k] = (lo[k] * (64 - w) + hi[k] * w + 32) >> 6;
         if (P) {
             int l1, cr1, cb1;
-            ycc(c[0], c[1], c[2], l1, cr1, cb1);
+            ycc_ramp(c[0], c[1], c[2], l1, cr1, cb1);
             tot += ycc_err(l1, cr1, cb1, tx.l(i), tx.cr(i), tx.cb(i), cf);
         } else {
             tot += wsq(c[0] - (int)ch(tex(px, i), 0), c[1] - (int)ch(tex(px, i), 1), c[2] - (int)ch(tex(px, i), 2), cf);
@@ -888,10 +997,12 @@ __device__ __forceinline__ uint32_t shape_mask(uint32_t shape, uint32_t subset)
 
 // estimate_partition :1207-1281
 template <bool P, class Y = Ycc>
-__device__ __forceinline__ uint32_t pick_partition(const uint32_t px[16], const Y &tx, const EncCfg &cf)
+__device__ __forceinline__ uint32_t pick_partition(const Y &tx, const EncCfg &cf)
 {
     const uint32_t total = cf.max_parts < 64 ? cf.max_parts : 64;
     if (total <= 1) return 0;
+    RegTex px;
+    px.load(tx);
     uint32_t best = kNone, best_part = 0, key = 0;
     bool stop = false;
     for (uint32_t it = 0; it < total; ++it) {
@@ -915,10 +1026,12 @@ __device__ __forceinline__ uint32_t pick_partition(const uint32_t px[16], const 
 // the reference's sequential choice (filter bank, stop rules, '<' keeps the
 // first) runs over those totals -- full sums are equivalent (see estimate2).
 template <bool P, class Y = Ycc>
-__device__ __forceinline__ uint32_t pick_partition_wave(const uint32_t px[16], const Y &tx, const EncCfg &cf)
+__device__ __forceinline__ uint32_t pick_partition_wave(const Y &tx, const EncCfg &cf)
 {
     const uint32_t total = cf.max_parts < 64 ? cf.max_parts : 64;
     if (total <= 1) return 0;
+    RegTex px;
+    px.load(tx);
     const uint32_t ln = threadIdx.x & 63u;
     uint32_t el = kNone;
     if (ln < total) el = estimate2<P>(shape_mask(kBc7Shape2[kEncPartOrder[ln]], 0), px, tx, cf, kNone);
@@ -1009,55 +1122,51 @@ __device__ __forceinline__ uint4 pack_block(bool mode1, uint32_t part, uint64_t 
 // :1390-1515 (m_endpoints_share_pbit, uninitialised for alpha blocks in the
 // reference, is false: mode 6 has a p-bit per endpoint)
 template <bool P, bool WAVE = false, class Y = Ycc>
-__device__ __forceinline__ uint4 encode_block(const uint32_t px[16], const EncCfg &cf, const EncLds &L, Y tx)
+__device__ __forceinline__ void encode_block(const uint32_t px[16], const EncCfg &cf, const EncLds &L, Y tx,
+                                             uint4 *out, bool writer)
 {
-    if (P) {
+    // the texels go to LDS (YccT / TexT); the register copy dies here
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            int l, cr, cb;
-            ycc(ch(tex(px, i), 0), ch(tex(px, i), 1), ch(tex(px, i), 2), l, cr, cb);
-            tx.put(i, l, cr, cb);
-        }
-    }
+    for (int i = 0; i < 16; ++i) tx.put(i, px[i]);
     bool alpha = false;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) alpha = alpha || (tex(px, i) >> 24) < 255u;
-    Res r6[1], r1[2];
-    bool mode1 = false;
-    uint32_t part = 0;
+    for (int i = 0; i < 16; ++i) alpha = alpha || (px[i] >> 24) < 255u;
+    uint32_t err6;
     {   // mode 6 on the whole block
         Prob p6[1];
+        Res r6[1];
         p6[0].mask = 0xffffu, p6[0].n = 16, p6[0].nsel = 16, p6[0].cbits = 7, p6[0].mode1 = false, p6[0].alpha = alpha;
-        cells<P, 1, Y, WAVE>(p6, 0xffffu, px, tx, cf, L, r6);
+        cells<P, 1, Y, WAVE>(p6, 0xffffu, tx, tx, cf, L, r6);
+        // the mode-6 block goes out now and is overwritten if mode 1 wins: only
+        // its error stays live through the mode-1 search (register budget)
+        const uint32_t lo[2] = {r6[0].lo, 0}, hi[2] = {r6[0].hi, 0};
+        uint32_t pb[2][2] = {{r6[0].pb0, r6[0].pb1}, {0, 0}};
+        const uint4 b6 = pack_block(false, 0, r6[0].sel, lo, hi, pb);
+        if (writer) *out = b6;
+        err6 = r6[0].err;
     }
-    if (!alpha && r6[0].err > 0 && cf.max_parts > 0) {
+    if (!alpha && err6 > 0 && cf.max_parts > 0) {
         // mode 1 on the partition the estimator picks, both subsets at once (the
         // reference stops after the first subset if it alone loses: equivalent)
-        part = WAVE ? pick_partition_wave<P>(px, tx, cf) : pick_partition<P>(px, tx, cf);
+        const uint32_t part = WAVE ? pick_partition_wave<P>(tx, cf) : pick_partition<P>(tx, cf);
         const uint32_t m0 = shape_mask(kBc7Shape2[part], 0);
         Prob p1[2];
+        Res r1[2];
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             p1[k].mask = k ? (~m0 & 0xffffu) : m0;
             p1[k].n = (uint32_t)__popc(p1[k].mask), p1[k].nsel = 8, p1[k].cbits = 6, p1[k].mode1 = true;
             p1[k].alpha = false;
         }
-        cells<P, 2, Y, WAVE>(p1, m0, px, tx, cf, L, r1);
-        mode1 = r1[0].err + r1[1].err < r6[0].err;
+        cells<P, 2, Y, WAVE>(p1, m0, tx, tx, cf, L, r1);
+        if (r1[0].err + r1[1].err < err6) {
+            // each subset's selectors sit in its own texels' nibbles
+            const uint32_t lo[2] = {r1[0].lo, r1[1].lo}, hi[2] = {r1[0].hi, r1[1].hi};
+            uint32_t pb[2][2] = {{r1[0].pb0, 0}, {r1[1].pb0, 0}};
+            const uint4 b1 = pack_block(true, part, r1[0].sel | r1[1].sel, lo, hi, pb);
+            if (writer) *out = b1;
+        }
     }
-    const Res s0 = r1[0], s1 = r1[1];
-    uint32_t lo[2], hi[2], pb[2][2];
-    uint64_t sel;
-    if (mode1) {
-        sel = s0.sel | s1.sel;   // each subset's selectors sit in its own texels' nibbles
-        lo[0] = s0.lo, hi[0] = s0.hi, pb[0][0] = s0.pb0, pb[0][1] = 0;
-        lo[1] = s1.lo, hi[1] = s1.hi, pb[1][0] = s1.pb0, pb[1][1] = 0;
-    } else {
-        sel = r6[0].sel;
-        lo[0] = r6[0].lo, hi[0] = r6[0].hi, pb[0][0] = r6[0].pb0, pb[0][1] = r6[0].pb1;
-        lo[1] = hi[1] = pb[1][0] = pb[1][1] = 0;
-    }
-    return pack_block(mode1, part, sel, lo, hi, pb);
 }
 
 // ---- kernels ---------------------------------------------------------------
@@ -1087,16 +1196,16 @@ __global__ void __launch_bounds__(256, GIC_ENC_WAVES) bc7enc_image_kernel(Geomet
                                                            uint4 *__restrict__ dst)
 {
     __shared__ EncLds L;
-    __shared__ int ytab[P ? 48 * kYccStride : 1];
+    __shared__ int ytab[TexSrc<P, kYccStride>::kRows * kYccStride];
     load_tables(L);
-    const Ycc tx{(uint32_t)(uintptr_t)(const __attribute__((address_space(3))) int *)(ytab + (P ? threadIdx.x : 0))};
+    const TexSrc<P, kYccStride> tx{(uint32_t)(uintptr_t)(const __attribute__((address_space(3))) int *)(ytab + threadIdx.x)};
     const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
     if (id >= g.total) return;
     uint32_t slice, by, bx;
     block_coords(g, id, slice, by, bx);
     uint32_t px[16];
     load_block_u8(g, slice, by, bx, force_alpha_one != 0, px);
-    dst[id] = encode_block<P>(px, cf, L, tx);
+    encode_block<P>(px, cf, L, tx, dst + id, true);
 }
 
 // Image_CompressRichGel999BC7enc16 :73-97: blocks of 16 packed RGBA8 words
@@ -1105,9 +1214,9 @@ __global__ void __launch_bounds__(256, GIC_ENC_WAVES) bc7enc_blocks_kernel(const
                                                             uint4 *__restrict__ dst)
 {
     __shared__ EncLds L;
-    __shared__ int ytab[P ? 48 * kYccStride : 1];
+    __shared__ int ytab[TexSrc<P, kYccStride>::kRows * kYccStride];
     load_tables(L);
-    const Ycc tx{(uint32_t)(uintptr_t)(const __attribute__((address_space(3))) int *)(ytab + (P ? threadIdx.x : 0))};
+    const TexSrc<P, kYccStride> tx{(uint32_t)(uintptr_t)(const __attribute__((address_space(3))) int *)(ytab + threadIdx.x)};
     const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
     if (id >= n) return;
     uint32_t px[16];
@@ -1116,7 +1225,7 @@ __global__ void __launch_bounds__(256, GIC_ENC_WAVES) bc7enc_blocks_kernel(const
         const uint4 v = blocks[(size_t)id * 4 + q];
         px[q * 4 + 0] = v.x, px[q * 4 + 1] = v.y, px[q * 4 + 2] = v.z, px[q * 4 + 3] = v.w;
     }
-    dst[id] = encode_block<P>(px, cf, L, tx);
+    encode_block<P>(px, cf, L, tx, dst + id, true);
 }
 
 // small batches (the block-level entry point): one block per 64-lane wave, the
@@ -1126,9 +1235,9 @@ __global__ void __launch_bounds__(64) bc7enc_blocks_wave_kernel(const uint4 *__r
                                                                 uint4 *__restrict__ dst)
 {
     __shared__ EncLds L;
-    __shared__ int ytab[P ? 48 * 64 : 1];
+    __shared__ int ytab[TexSrc<P, 64>::kRows * 64];
     load_tables(L);
-    const YccT<64> tx{(uint32_t)(uintptr_t)(const __attribute__((address_space(3))) int *)(ytab + (P ? threadIdx.x : 0))};
+    const TexSrc<P, 64> tx{(uint32_t)(uintptr_t)(const __attribute__((address_space(3))) int *)(ytab + threadIdx.x)};
     const uint32_t id = blockIdx.x;
     if (id >= n) return;
     uint32_t px[16];
@@ -1137,8 +1246,7 @@ __global__ void __launch_bounds__(64) bc7enc_blocks_wave_kernel(const uint4 *__r
         const uint4 v = blocks[(size_t)id * 4 + q];
         px[q * 4 + 0] = v.x, px[q * 4 + 1] = v.y, px[q * 4 + 2] = v.z, px[q * 4 + 3] = v.w;
     }
-    const uint4 b = encode_block<P, true>(px, cf, L, tx);
-    if (threadIdx.x == 0) dst[id] = b;
+    encode_block<P, true>(px, cf, L, tx, dst + id, threadIdx.x == 0);
 }
 
 // float RGBA blocks (the gic_hip_encode_rows_src / block-ABI path): each texel
@@ -1149,9 +1257,9 @@ __global__ void __launch_bounds__(256, GIC_ENC_WAVES) bc7enc_f32_kernel(const fl
                                                          uint4 *__restrict__ dst)
 {
     __shared__ EncLds L;
-    __shared__ int ytab[P ? 48 * kYccStride : 1];
+    __shared__ int ytab[TexSrc<P, kYccStride>::kRows * kYccStride];
     load_tables(L);
-    const Ycc tx{(uint32_t)(uintptr_t)(const __attribute__((address_space(3))) int *)(ytab + (P ? threadIdx.x : 0))};
+    const TexSrc<P, kYccStride> tx{(uint32_t)(uintptr_t)(const __attribute__((address_space(3))) int *)(ytab + threadIdx.x)};
     const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
     if (id >= n) return;
     uint32_t px[16];
@@ -1165,7 +1273,7 @@ __global__ void __launch_bounds__(256, GIC_ENC_WAVES) bc7enc_f32_kernel(const fl
         for (int k = 0; k < 4; ++k) w |= (uint32_t)(sat(c[k]) * 255.0f + 0.5f) << (8 * k);
         px[t] = w;
     }
-    dst[id] = encode_block<P>(px, cf, L, tx);
+    encode_block<P>(px, cf, L, tx, dst + id, true);
 }
 
 EncCfg make_cfg(const gic_options &o)

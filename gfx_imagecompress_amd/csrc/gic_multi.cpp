@@ -230,7 +230,6 @@ extern "C" int gic_encode_multi(gic_format fmt, gic_source src_type, const void 
     t_report.rccl = rccl ? 1 : 0;
 
     const gic::EncodeArgs args{fmt, src_type, width, height, channels, row_pitch, opt};
-    const uint32_t per = gic::piece_rows(fmt, bx);
     std::vector<gic::LaneJob> jobs(ndev);
     std::vector<double> encoded_at(ndev, 0.0);
     const double t0 = gic::now_ms();
@@ -247,7 +246,7 @@ extern "C" int gic_encode_multi(gic_format fmt, gic_source src_type, const void 
         if (grow(r.src, r.src_cap, gic::slab_bytes(first, n, by, height, row_pitch)) != hipSuccess) return GIC_EHIP;
         if (i && grow(r.dst, r.dst_cap, n * row_bytes) != hipSuccess) return GIC_EHIP;
         uint8_t *out = i ? r.dst : d_dst_root + first * row_bytes;
-        j.pieces = gic::make_pieces(first, n, per, by, height, row_pitch, row_bytes, (const uint8_t *)h_src, r.src,
+        j.pieces = gic::make_pieces(first, n, gic::piece_plan(fmt, bx, n), by, height, row_pitch, row_bytes, (const uint8_t *)h_src, r.src,
                                     out, nullptr);
         if (!i) {
             j.after = [&, i] {
@@ -351,7 +350,6 @@ int encode_host(const std::vector<LaneBuffers *> &lanes, const EncodeArgs &a, co
     const uint64_t rows_total = (uint64_t)by * slices;
     const size_t row_bytes = (size_t)bx * bb;
     const int n = (int)lanes.size();
-    const uint32_t per = piece_rows(a.fmt, bx);
     std::vector<LaneJob> jobs(n);
     for (int i = 0; i < n; ++i) {
         uint64_t first = 0, rows = 0;
@@ -363,7 +361,7 @@ int encode_host(const std::vector<LaneBuffers *> &lanes, const EncodeArgs &a, co
         if (!rows) continue;
         if (lanes[i]->reserve(slab_bytes(first, rows, by, a.height, a.row_pitch), rows * row_bytes) != hipSuccess)
             return GIC_EHIP;
-        j.pieces = make_pieces(first, rows, per, by, a.height, a.row_pitch, row_bytes, h_src, lanes[i]->src,
+        j.pieces = make_pieces(first, rows, piece_plan(a.fmt, bx, rows), by, a.height, a.row_pitch, row_bytes, h_src, lanes[i]->src,
                                lanes[i]->dst, h_out + first * row_bytes);
     }
     const int rc = drive(jobs, a, bx, by, cb, user);

@@ -33,6 +33,7 @@ hipError_t Lane::init(int dev)
     hipError_t e = hipSetDevice(dev);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&up, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&enc, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&enc2, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&down, hipStreamNonBlocking);
     for (hipEvent_t *t : {&t_up0, &t_up1, &t_enc0, &t_enc1, &t_dn0, &t_dn1})
         if (e == hipSuccess) e = hipEventCreate(t);
@@ -54,6 +55,20 @@ hipError_t Lane::reserve_events(size_t pieces)
         ev_up.push_back(a);
         ev_enc.push_back(b);
     }
+    return e;
+}
+
+hipError_t Lane::reserve_down(size_t slot_bytes)
+{
+    hipError_t e = hipSuccess;
+    for (hipEvent_t *ev : {&ev_dn[0], &ev_dn[1]})
+        if (e == hipSuccess && !*ev) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+    if (e != hipSuccess || slot_bytes <= dstage_slot) return e;
+    if (dstage) (void)hipHostFree(dstage);
+    dstage = nullptr;
+    dstage_slot = 0;
+    e = hipHostMalloc((void **)&dstage, slot_bytes * 2, hipHostMallocDefault);
+    if (e == hipSuccess) dstage_slot = slot_bytes;
     return e;
 }
 
@@ -79,23 +94,35 @@ void Lane::release()
         if (*t) (void)hipEventDestroy(*t);
         *t = nullptr;
     }
-    for (hipStream_t *s : {&up, &enc, &down}) {
+    for (hipStream_t *s : {&up, &enc, &enc2, &down}) {
         if (*s) (void)hipStreamDestroy(*s);
         *s = nullptr;
     }
     if (stage) (void)hipHostFree(stage);
     stage = nullptr;
     stage_slot = 0;
+    if (dstage) (void)hipHostFree(dstage);
+    dstage = nullptr;
+    dstage_slot = 0;
+    for (hipEvent_t *ev : {&ev_dn[0], &ev_dn[1]}) {
+        if (*ev) (void)hipEventDestroy(*ev);
+        *ev = nullptr;
+    }
     device = -1;
 }
 
-uint32_t piece_rows(gic_format fmt, uint32_t blocks_x)
+PiecePlan piece_plan(gic_format fmt, uint32_t blocks_x, uint64_t rows)
 {
-    uint64_t target = fmt == GIC_FMT_BC7 ? (1u << 20) : (1u << 18);
+    const uint64_t bx = blocks_x ? blocks_x : 1;
+    auto clamp_rows = [](uint64_t r) { return r < 1 ? 1u : (r > 0xffffffffull ? 0xffffffffu : (uint32_t)r); };
     const char *e = getenv("GIC_PIECE_BLOCKS");   // test / tuning hook
-    if (e && atoll(e) > 0) target = (uint64_t)atoll(e);
-    const uint64_t r = target / (blocks_x ? blocks_x : 1);
-    return r < 1 ? 1u : (r > 0xffffffffull ? 0xffffffffu : (uint32_t)r);
+    if (e && atoll(e) > 0) {
+        const uint32_t r = clamp_rows((uint64_t)atoll(e) / bx);
+        return PiecePlan{r, r};
+    }
+    if (fmt == GIC_FMT_BC7) return PiecePlan{clamp_rows(rows / 16), 0xffffffffu};
+    const uint32_t r = clamp_rows((1u << 18) / bx);
+    return PiecePlan{r, r};
 }
 
 size_t slab_bytes(uint64_t first, uint64_t rows, uint32_t by, uint32_t height, size_t pitch)
@@ -112,7 +139,7 @@ size_t slab_bytes(uint64_t first, uint64_t rows, uint32_t by, uint32_t height, s
     return bytes;
 }
 
-std::vector<Piece> make_pieces(uint64_t first, uint64_t rows, uint32_t per, uint32_t by, uint32_t height,
+std::vector<Piece> make_pieces(uint64_t first, uint64_t rows, const PiecePlan &plan, uint32_t by, uint32_t height,
                                size_t pitch, size_t row_bytes, const uint8_t *h_src, uint8_t *d_slab, uint8_t *d_out,
                                uint8_t *h_out)
 {
@@ -122,6 +149,7 @@ std::vector<Piece> make_pieces(uint64_t first, uint64_t rows, uint32_t per, uint
     for (uint64_t row = first, end = first + rows; row < end;) {
         const uint32_t w = (uint32_t)(row / by), y0 = (uint32_t)(row % by);
         uint64_t n = by - y0;
+        const uint32_t per = out.empty() ? plan.first : plan.per;
         if (n > per) n = per;
         if (n > end - row) n = end - row;
         const uint32_t py1 = 4 * (y0 + n) < height ? (uint32_t)(4 * (y0 + n)) : height;
@@ -213,6 +241,9 @@ int run_pieces(Lane &lane, const EncodeArgs &a, const std::vector<Piece> &pieces
     size_t max_src = 0;
     for (const Piece &p : pieces) max_src = p.src_bytes > max_src ? p.src_bytes : max_src;
     if (e == hipSuccess && mode == H2D::Staged) e = lane.reserve_stage(max_src);
+    size_t max_out = 0;
+    for (const Piece &p : pieces) max_out = p.h_out && p.out_bytes > max_out ? p.out_bytes : max_out;
+    if (e == hipSuccess && max_out) e = lane.reserve_down(max_out);
     Registration reg;
     if (e == hipSuccess && mode == H2D::Register) {
         // pieces of one lane read one contiguous host range (slices are stacked)
@@ -250,9 +281,23 @@ int run_pieces(Lane &lane, const EncodeArgs &a, const std::vector<Piece> &pieces
         uploaded.fail();   // wakes the encoder if it waits past the last posted piece
     });
 
+    // Downloads go through a pinned two-slot ring: the device-to-pinned copy is
+    // an SDMA transfer, where a copy to pageable memory is a blit kernel that
+    // waits for free CUs -- behind the encode kernels, i.e. after the last one
+    // (the rocprofv3 trace of round 6, profiles/r06_host_pipeline_trace.txt) --
+    // and the CPU copy of piece k into the caller's image overlaps the transfer
+    // of piece k+1.
     std::thread downloader([&] {
         hipError_t err = hipSetDevice(lane.device);
         bool first = true;
+        size_t pend = (size_t)-1;   // the piece whose transfer is in flight
+        auto finish = [&](size_t k) {   // piece k's transfer done: into the image
+            const Piece &p = pieces[k];
+            hipError_t e2 = hipEventSynchronize(lane.ev_dn[k & 1]);
+            if (e2 == hipSuccess) memcpy(p.h_out, lane.dstage + (k & 1) * lane.dstage_slot, p.out_bytes);
+            if (e2 == hipSuccess && progress) progress->add(lane_index, p.n);
+            return e2;
+        };
         for (size_t k = 0; k < pieces.size() && err == hipSuccess; ++k) {
             if (!encoded.wait(k)) break;
             const Piece &p = pieces[k];
@@ -261,41 +306,56 @@ int run_pieces(Lane &lane, const EncodeArgs &a, const std::vector<Piece> &pieces
                 if (err == hipSuccess && first) err = hipEventRecord(lane.t_dn0, lane.down);
                 first = false;
                 if (err == hipSuccess)
-                    err = hipMemcpyAsync(p.h_out, p.d_out, p.out_bytes, hipMemcpyDeviceToHost, lane.down);
-                if (err == hipSuccess) err = hipStreamSynchronize(lane.down);
+                    err = hipMemcpyAsync(lane.dstage + (k & 1) * lane.dstage_slot, p.d_out, p.out_bytes,
+                                         hipMemcpyDeviceToHost, lane.down);
+                if (err == hipSuccess) err = hipEventRecord(lane.ev_dn[k & 1], lane.down);
+                if (err == hipSuccess && pend != (size_t)-1) err = finish(pend);
+                pend = k;
             } else {
                 err = hipEventSynchronize(lane.ev_enc[k]);
+                if (err == hipSuccess && progress) progress->add(lane_index, p.n);
             }
-            if (err == hipSuccess && progress) progress->add(lane_index, p.n);
         }
+        if (err == hipSuccess && pend != (size_t)-1) err = finish(pend);
         if (err == hipSuccess && !first) err = hipEventRecord(lane.t_dn1, lane.down);
         if (err == hipSuccess && !first) err = hipStreamSynchronize(lane.down);
         e_dn = err;
     });
 
+    // consecutive pieces alternate between the lane's two encode streams (BC7
+    // calls complete before they return, so BC7 keeps one)
+    const int nstreams = a.fmt == GIC_FMT_BC7 ? 1 : 2;
+    const hipStream_t es[2] = {lane.enc, lane.enc2};
     int rc = GIC_OK;
     size_t issued = 0;
     for (size_t k = 0; k < pieces.size() && !stop(); ++k) {
         if (!uploaded.wait(k)) break;
         const Piece &p = pieces[k];
-        e = hipStreamWaitEvent(lane.enc, lane.ev_up[k], 0);
-        if (e == hipSuccess && k == 0) e = hipEventRecord(lane.t_enc0, lane.enc);
+        const hipStream_t s = es[k % nstreams];
+        e = hipStreamWaitEvent(s, lane.ev_up[k], 0);
+        if (e == hipSuccess && k == 0) e = hipEventRecord(lane.t_enc0, s);
         if (e != hipSuccess) break;
         rc = gic_hip_encode_rows_src(a.fmt, a.src_type, p.d_slice, a.width, a.height, 1, a.channels, a.row_pitch,
-                                     p.y0, p.n, a.opt, p.d_out, nullptr, lane.enc);
+                                     p.y0, p.n, a.opt, p.d_out, nullptr, s);
         if (rc != GIC_OK) break;
-        e = hipEventRecord(lane.ev_enc[k], lane.enc);
+        e = hipEventRecord(lane.ev_enc[k], s);
         if (e != hipSuccess) break;
         issued = k + 1;
         encoded.post(issued);
+    }
+    if (issued > 1 && nstreams > 1 && e == hipSuccess) {   // join: stream 0 waits for stream 1's last piece
+        const size_t last1 = (issued - 1) % 2 == 1 ? issued - 1 : issued - 2;
+        e = hipStreamWaitEvent(lane.enc, lane.ev_enc[last1], 0);
     }
     if (issued && e == hipSuccess) e = hipEventRecord(lane.t_enc1, lane.enc);
     encoded.fail();
     if (rc != GIC_OK || e != hipSuccess) halt.store(true);   // the uploader stops at its next piece
     uploader.join();
     downloader.join();
-    const hipError_t es = hipStreamSynchronize(lane.enc);
-    if (e == hipSuccess) e = es;
+    hipError_t ee = hipStreamSynchronize(lane.enc);
+    if (e == hipSuccess) e = ee;
+    ee = hipStreamSynchronize(lane.enc2);
+    if (e == hipSuccess) e = ee;
     const hipError_t eu = hipStreamSynchronize(lane.up);
     if (e_up == hipSuccess) e_up = eu;
     if (rc != GIC_OK) return rc;

@@ -9,8 +9,12 @@
 //   upload   (a helper thread, running ahead: piece k+1 crosses PCIe while
 //             piece k encodes),
 //   encode   (the calling thread, gic_hip_encode_rows_src on the lane's
-//             encode stream, each piece waiting on its own upload event),
-//   download (a helper thread: piece k's blocks come back while k+1 encodes).
+//             encode streams, each piece waiting on its own upload event;
+//             consecutive pieces alternate between two streams, so the tail of
+//             one launch overlaps the next -- 16 pieces of an 8K BC1 image
+//             then cost what one launch does, profiles/r06_pieces.txt),
+//   download (a helper thread: piece k's blocks come back while k+1 encodes,
+//             through pinned slots -- an SDMA transfer, not a blit kernel).
 // Stages hand pieces over through per-piece events and counters; every event,
 // stream and staging buffer belongs to the lane and is reused across calls.
 #pragma once
@@ -62,15 +66,19 @@ struct EncodeArgs {
 // Per-device streams, events and pinned staging, reused across calls.
 struct Lane {
     int device = -1;
-    hipStream_t up = nullptr, enc = nullptr, down = nullptr;
+    hipStream_t up = nullptr, enc = nullptr, enc2 = nullptr, down = nullptr;
     std::vector<hipEvent_t> ev_up, ev_enc;              // one per piece (grown on demand)
     hipEvent_t t_up0 = nullptr, t_up1 = nullptr, t_enc0 = nullptr, t_enc1 = nullptr, t_dn0 = nullptr,
                t_dn1 = nullptr;                          // stage spans (timing)
     uint8_t *stage = nullptr;                            // pinned ring (H2D::Staged)
     size_t stage_slot = 0;
+    uint8_t *dstage = nullptr;                           // pinned two-slot ring of the downloads
+    size_t dstage_slot = 0;
+    hipEvent_t ev_dn[2] = {nullptr, nullptr};
     hipError_t init(int dev);
     hipError_t reserve_events(size_t pieces);
     hipError_t reserve_stage(size_t slot_bytes);
+    hipError_t reserve_down(size_t slot_bytes);
     void release();
 };
 
@@ -112,19 +120,25 @@ struct StageTimes {
 int run_pieces(Lane &lane, const EncodeArgs &a, const std::vector<Piece> &pieces, Progress *progress, int lane_index,
                StageTimes *times);
 
-// Block rows per piece for a format: about 2^18 blocks (BC7: 2^20, its calls
-// run a multi-stage pipeline of their own); GIC_PIECE_BLOCKS overrides the
-// block count (tests, tuning).
-uint32_t piece_rows(gic_format fmt, uint32_t blocks_x);
+// Block rows per piece: `first` for the first piece of a range, `per` for
+// the others.  The lane-per-block kernels take about 2^18 blocks a piece (their
+// launches overlap on two streams, so small pieces cost nothing and the first
+// upload is short); BC7 calls carry a multi-stage pipeline of their own and
+// lose 5-15 % per extra call (profiles/r06_pieces.txt), so BC7 takes a small
+// first piece (1/16 of the range: its upload is all the encode waits for) and
+// the rest in one.  GIC_PIECE_BLOCKS overrides both with a block count (tests).
+struct PiecePlan {
+    uint32_t first, per;
+};
+PiecePlan piece_plan(gic_format fmt, uint32_t blocks_x, uint64_t rows);
 
-// Cuts the slice-major block rows [first, first + rows) into pieces of at most
-// `per` rows that do not cross slices.  Source bytes come from h_src (slices x
-// height rows of pitch bytes) and land in d_src_slab packed in order; each
-// piece's blocks go to d_out + (row - first) * row_bytes (and h_out likewise,
-// if not null).
-std::vector<Piece> make_pieces(uint64_t first, uint64_t rows, uint32_t per, uint32_t blocks_y, uint32_t height,
-                               size_t pitch, size_t row_bytes, const uint8_t *h_src, uint8_t *d_src_slab,
-                               uint8_t *d_out, uint8_t *h_out);
+// Cuts the slice-major block rows [first, first + rows) into pieces (plan)
+// that do not cross slices.  Source bytes come from h_src (slices x height rows
+// of pitch bytes) and land in d_src_slab packed in order; each piece's blocks
+// go to d_out + (row - first) * row_bytes (and h_out likewise, if not null).
+std::vector<Piece> make_pieces(uint64_t first, uint64_t rows, const PiecePlan &plan, uint32_t blocks_y,
+                               uint32_t height, size_t pitch, size_t row_bytes, const uint8_t *h_src,
+                               uint8_t *d_src_slab, uint8_t *d_out, uint8_t *h_out);
 // the source bytes make_pieces lays out for that range
 size_t slab_bytes(uint64_t first, uint64_t rows, uint32_t blocks_y, uint32_t height, size_t pitch);
 
