@@ -35,7 +35,7 @@ hipError_t Lane::init(int dev)
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&enc, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&enc2, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&down, hipStreamNonBlocking);
-    for (hipEvent_t *t : {&t_up0, &t_up1, &t_enc0, &t_enc1, &t_dn0, &t_dn1})
+    for (hipEvent_t *t : {&t_up0, &t_up1, &t_enc0, &t_enc1})
         if (e == hipSuccess) e = hipEventCreate(t);
     if (e != hipSuccess) release();
     return e;
@@ -58,17 +58,14 @@ hipError_t Lane::reserve_events(size_t pieces)
     return e;
 }
 
-hipError_t Lane::reserve_down(size_t slot_bytes)
+hipError_t Lane::reserve_zc(size_t bytes)
 {
-    hipError_t e = hipSuccess;
-    for (hipEvent_t *ev : {&ev_dn[0], &ev_dn[1]})
-        if (e == hipSuccess && !*ev) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
-    if (e != hipSuccess || slot_bytes <= dstage_slot) return e;
-    if (dstage) (void)hipHostFree(dstage);
-    dstage = nullptr;
-    dstage_slot = 0;
-    e = hipHostMalloc((void **)&dstage, slot_bytes * 2, hipHostMallocDefault);
-    if (e == hipSuccess) dstage_slot = slot_bytes;
+    if (bytes <= zc_cap) return hipSuccess;
+    if (zc) (void)hipHostFree(zc);
+    zc = nullptr;
+    zc_cap = 0;
+    const hipError_t e = hipHostMalloc((void **)&zc, bytes, hipHostMallocDefault);
+    if (e == hipSuccess) zc_cap = bytes;
     return e;
 }
 
@@ -90,7 +87,7 @@ void Lane::release()
     for (hipEvent_t ev : ev_enc) (void)hipEventDestroy(ev);
     ev_up.clear();
     ev_enc.clear();
-    for (hipEvent_t *t : {&t_up0, &t_up1, &t_enc0, &t_enc1, &t_dn0, &t_dn1}) {
+    for (hipEvent_t *t : {&t_up0, &t_up1, &t_enc0, &t_enc1}) {
         if (*t) (void)hipEventDestroy(*t);
         *t = nullptr;
     }
@@ -101,13 +98,9 @@ void Lane::release()
     if (stage) (void)hipHostFree(stage);
     stage = nullptr;
     stage_slot = 0;
-    if (dstage) (void)hipHostFree(dstage);
-    dstage = nullptr;
-    dstage_slot = 0;
-    for (hipEvent_t *ev : {&ev_dn[0], &ev_dn[1]}) {
-        if (*ev) (void)hipEventDestroy(*ev);
-        *ev = nullptr;
-    }
+    if (zc) (void)hipHostFree(zc);
+    zc = nullptr;
+    zc_cap = 0;
     device = -1;
 }
 
@@ -241,9 +234,15 @@ int run_pieces(Lane &lane, const EncodeArgs &a, const std::vector<Piece> &pieces
     size_t max_src = 0;
     for (const Piece &p : pieces) max_src = p.src_bytes > max_src ? p.src_bytes : max_src;
     if (e == hipSuccess && mode == H2D::Staged) e = lane.reserve_stage(max_src);
-    size_t max_out = 0;
-    for (const Piece &p : pieces) max_out = p.h_out && p.out_bytes > max_out ? p.out_bytes : max_out;
-    if (e == hipSuccess && max_out) e = lane.reserve_down(max_out);
+    // zero-copy outputs (see the download stage): piece k at zc + zc_off[k]
+    std::vector<size_t> zc_off(pieces.size(), 0);
+    size_t zc_bytes = 0;
+    for (size_t k = 0; k < pieces.size(); ++k) {
+        zc_off[k] = zc_bytes;
+        if (pieces[k].h_out) zc_bytes += pieces[k].out_bytes;
+    }
+    if (e == hipSuccess && zc_bytes) e = lane.reserve_zc(zc_bytes);
+    double d2h_span = 0;
     Registration reg;
     if (e == hipSuccess && mode == H2D::Register) {
         // pieces of one lane read one contiguous host range (slices are stacked)
@@ -281,44 +280,28 @@ int run_pieces(Lane &lane, const EncodeArgs &a, const std::vector<Piece> &pieces
         uploaded.fail();   // wakes the encoder if it waits past the last posted piece
     });
 
-    // Downloads go through a pinned two-slot ring: the device-to-pinned copy is
-    // an SDMA transfer, where a copy to pageable memory is a blit kernel that
-    // waits for free CUs -- behind the encode kernels, i.e. after the last one
-    // (the rocprofv3 trace of round 6, profiles/r06_host_pipeline_trace.txt) --
-    // and the CPU copy of piece k into the caller's image overlaps the transfer
-    // of piece k+1.
+    // Pieces with a host destination are encoded straight into pinned host
+    // memory (the kernels' block stores cross PCIe as they retire), and the
+    // download stage only copies each finished piece into the caller's image.
+    // A device-to-host copy would be a blit kernel, and that waits for free CUs
+    // -- behind every queued encode kernel, i.e. after the last one (rocprofv3
+    // trace of round 6, profiles/r06_host_pipeline_trace.txt).
     std::thread downloader([&] {
         hipError_t err = hipSetDevice(lane.device);
-        bool first = true;
-        size_t pend = (size_t)-1;   // the piece whose transfer is in flight
-        auto finish = [&](size_t k) {   // piece k's transfer done: into the image
-            const Piece &p = pieces[k];
-            hipError_t e2 = hipEventSynchronize(lane.ev_dn[k & 1]);
-            if (e2 == hipSuccess) memcpy(p.h_out, lane.dstage + (k & 1) * lane.dstage_slot, p.out_bytes);
-            if (e2 == hipSuccess && progress) progress->add(lane_index, p.n);
-            return e2;
-        };
+        double t0 = 0, t1 = 0;
         for (size_t k = 0; k < pieces.size() && err == hipSuccess; ++k) {
             if (!encoded.wait(k)) break;
             const Piece &p = pieces[k];
-            if (p.h_out) {
-                err = hipStreamWaitEvent(lane.down, lane.ev_enc[k], 0);
-                if (err == hipSuccess && first) err = hipEventRecord(lane.t_dn0, lane.down);
-                first = false;
-                if (err == hipSuccess)
-                    err = hipMemcpyAsync(lane.dstage + (k & 1) * lane.dstage_slot, p.d_out, p.out_bytes,
-                                         hipMemcpyDeviceToHost, lane.down);
-                if (err == hipSuccess) err = hipEventRecord(lane.ev_dn[k & 1], lane.down);
-                if (err == hipSuccess && pend != (size_t)-1) err = finish(pend);
-                pend = k;
-            } else {
-                err = hipEventSynchronize(lane.ev_enc[k]);
-                if (err == hipSuccess && progress) progress->add(lane_index, p.n);
+            err = hipEventSynchronize(lane.ev_enc[k]);
+            if (err == hipSuccess && p.h_out) {
+                const double t = now_ms();
+                if (t0 == 0) t0 = t;
+                memcpy(p.h_out, lane.zc + zc_off[k], p.out_bytes);
+                t1 = now_ms();
             }
+            if (err == hipSuccess && progress) progress->add(lane_index, p.n);
         }
-        if (err == hipSuccess && pend != (size_t)-1) err = finish(pend);
-        if (err == hipSuccess && !first) err = hipEventRecord(lane.t_dn1, lane.down);
-        if (err == hipSuccess && !first) err = hipStreamSynchronize(lane.down);
+        d2h_span = t1 - t0;
         e_dn = err;
     });
 
@@ -336,7 +319,7 @@ int run_pieces(Lane &lane, const EncodeArgs &a, const std::vector<Piece> &pieces
         if (e == hipSuccess && k == 0) e = hipEventRecord(lane.t_enc0, s);
         if (e != hipSuccess) break;
         rc = gic_hip_encode_rows_src(a.fmt, a.src_type, p.d_slice, a.width, a.height, 1, a.channels, a.row_pitch,
-                                     p.y0, p.n, a.opt, p.d_out, nullptr, s);
+                                     p.y0, p.n, a.opt, p.h_out ? lane.zc + zc_off[k] : p.d_out, nullptr, s);
         if (rc != GIC_OK) break;
         e = hipEventRecord(lane.ev_enc[k], s);
         if (e != hipSuccess) break;
@@ -363,9 +346,7 @@ int run_pieces(Lane &lane, const EncodeArgs &a, const std::vector<Piece> &pieces
     if (times && issued == pieces.size()) {
         times->h2d_ms = span_ms(lane.t_up0, lane.t_up1);
         times->encode_ms = span_ms(lane.t_enc0, lane.t_enc1);
-        bool any_dn = false;
-        for (const Piece &p : pieces) any_dn = any_dn || p.h_out;
-        times->d2h_ms = any_dn ? span_ms(lane.t_dn0, lane.t_dn1) : 0.0;
+        times->d2h_ms = d2h_span;
     }
     return GIC_OK;
 }

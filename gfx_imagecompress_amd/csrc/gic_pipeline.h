@@ -13,8 +13,9 @@
 //             consecutive pieces alternate between two streams, so the tail of
 //             one launch overlaps the next -- 16 pieces of an 8K BC1 image
 //             then cost what one launch does, profiles/r06_pieces.txt),
-//   download (a helper thread: piece k's blocks come back while k+1 encodes,
-//             through pinned slots -- an SDMA transfer, not a blit kernel).
+//   download (a helper thread: the kernels write a host image's blocks straight
+//             into pinned host memory; piece k is copied into the image while
+//             k+1 encodes).
 // Stages hand pieces over through per-piece events and counters; every event,
 // stream and staging buffer belongs to the lane and is reused across calls.
 #pragma once
@@ -68,17 +69,15 @@ struct Lane {
     int device = -1;
     hipStream_t up = nullptr, enc = nullptr, enc2 = nullptr, down = nullptr;
     std::vector<hipEvent_t> ev_up, ev_enc;              // one per piece (grown on demand)
-    hipEvent_t t_up0 = nullptr, t_up1 = nullptr, t_enc0 = nullptr, t_enc1 = nullptr, t_dn0 = nullptr,
-               t_dn1 = nullptr;                          // stage spans (timing)
+    hipEvent_t t_up0 = nullptr, t_up1 = nullptr, t_enc0 = nullptr, t_enc1 = nullptr;   // stage spans (timing)
     uint8_t *stage = nullptr;                            // pinned ring (H2D::Staged)
     size_t stage_slot = 0;
-    uint8_t *dstage = nullptr;                           // pinned two-slot ring of the downloads
-    size_t dstage_slot = 0;
-    hipEvent_t ev_dn[2] = {nullptr, nullptr};
+    uint8_t *zc = nullptr;                               // pinned outputs the kernels write (host images)
+    size_t zc_cap = 0;
     hipError_t init(int dev);
     hipError_t reserve_events(size_t pieces);
     hipError_t reserve_stage(size_t slot_bytes);
-    hipError_t reserve_down(size_t slot_bytes);
+    hipError_t reserve_zc(size_t bytes);
     void release();
 };
 
@@ -109,7 +108,8 @@ struct Progress {
 };
 
 struct StageTimes {
-    double h2d_ms = 0, encode_ms = 0, d2h_ms = 0;   // first start -> last end of each stage (HIP events)
+    double h2d_ms = 0, encode_ms = 0;   // first start -> last end of each stage (HIP events)
+    double d2h_ms = 0;                  // first -> last copy into the host image (host clock)
 };
 
 // Runs `pieces` (in order) through `lane` on the calling thread plus two helper

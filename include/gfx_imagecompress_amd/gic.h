@@ -164,7 +164,7 @@ int gic_multi_split(uint64_t rows_total, int ndev, int i, uint64_t *first, uint6
 /* Host images (the Image_Compress* entry points and gic_compress_image).  The
  * reference's wrappers take a host image and return one (amd_bc1_compressor.cpp:
  * 36-70); here the block rows are cut into pieces (about 2^18 blocks, BC7 2^20)
- * and each device pipelines them: the upload of piece k+1 and the download of
+ * and each device pipelines them: the upload of piece k+1 and the copy-out of
  * piece k-1 overlap the encode of piece k (gic_pipeline.cpp).  The upload mode
  * is the environment variable GIC_H2D: "pageable" (default: hipMemcpyAsync from
  * the caller's memory), "staged" (through a pinned ring) or "register"
@@ -180,7 +180,8 @@ typedef struct gic_host_report {
     double total_ms;   /* the whole call, host clock */
     double h2d_ms;     /* first upload start -> last upload end (HIP events; the slowest device) */
     double encode_ms;  /* first encode start -> last encode end */
-    double d2h_ms;     /* first download start -> last download end */
+    double d2h_ms;     /* first -> last copy of finished blocks into the host image (host clock; the
+                          kernels write a host image's blocks straight into pinned host memory) */
 } gic_host_report;
 /* the calling thread's last host-image call */
 int gic_last_host_report(gic_host_report *out);
