@@ -262,10 +262,12 @@ __device__ __forceinline__ unsigned wave_minu(unsigned v)
 // a non-negative, non-NaN e (+inf for "no candidate": the NaN-rejecting tests sit
 // before the call) and o >= 0, so float order is the bit patterns' unsigned
 // order and the minimum does not depend on the reduction order: two DPP
-// minima instead of six rounds of two ds_bpermute shuffles.
+// minima instead of six rounds of two ds_bpermute shuffles.  e + 0.0f maps -0
+// to +0 (round to nearest; the build has no fast-math) so a -0 ties with +0 and
+// the lower o wins, as a float compare would have it.
 __device__ __forceinline__ void wave_argmin(float &e, int &o)
 {
-    const unsigned eb = __float_as_uint(e);
+    const unsigned eb = __float_as_uint(e + 0.0f);
     const unsigned emin = wave_minu(eb);
     const unsigned om = wave_minu(eb == emin ? (unsigned)o : 0xffffffffu);
     e = __uint_as_float(emin);

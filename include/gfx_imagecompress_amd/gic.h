@@ -275,7 +275,10 @@ int gic_block_last_status(void);
  *    cyclic stops and is counted as non-terminating.
  *  - BC6H: each loop stops at a proven cycle (non-terminating) or after `cap`
  *    rounds past the exhaustion within that loop (counted as a cap stop); the
- *    oracle (oracle/orc_bc6h.c) applies the same stops.
+ *    oracle (oracle/orc_bc6h.c) applies the same stops.  For BC6H both counters
+ *    count loops per EXECUTED outer round: a proven outer-round cycle is
+ *    fast-forwarded without running the skipped rounds' loops, so read the
+ *    BC6H counts as a 0 / non-zero signal, not as the oracle's loop totals.
  *   gic_iter_cap_hits: cap stops since the last reset on the current device
  *     (synchronises the device); a BC7 stop means a re-run, not a wrong block;
  *   gic_set_iter_cap: the cap (< 0 restores 4096; a small cap is a test hook);
