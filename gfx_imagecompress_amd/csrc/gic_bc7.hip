@@ -1717,6 +1717,159 @@ __global__ void __launch_bounds__(256) k_quant_probe6(Params p, Workspace ws)
     ws.qidx[(size_t)b * kQuantTasks + 208] = tidx;
 }
 
+// Bounded exit, stage 0 (round 6; not the reference's search): a mode-6 block
+// straight from the quantiser's first projection -- least-squares endpoints for
+// BC7's 4-bit interpolation weights, both endpoints' 7-bit codes and parity
+// bits chosen jointly by the error of the resulting palette (every texel taken
+// to its nearest entry), then one refit from those indices, the better of the
+// two kept.  Final when the packed block decodes within the bound, like a probe:
+// it only decides which blocks skip the later stages, and a final block meets
+// the contract by the bound.  Modelled bit for bit by oracle/orc_bc7.c
+// orc_bc7_fit6 (integer sums, the same f64 solve and rounding).  On 8K G1 it
+// finishes about as many blocks as the mode-6 shaker probe did, for a fraction
+// of the cost, and the shaker probe then runs over the few percent it leaves.
+__constant__ int kW16[16] = {0, 4, 9, 13, 17, 21, 26, 30, 34, 38, 43, 47, 51, 55, 60, 64};
+
+// palette of endpoint values q0, q1 (8-bit, parity included) and the texels'
+// nearest entries (first of least error, 4 bits per texel); returns the summed
+// squared error.  Palette entry outer, texel inner: each entry is formed once
+// and every texel keeps its running minimum (no 16-entry palette held live).
+__device__ __forceinline__ uint32_t fit6_palette(const uint32_t px[16], const int q0[4], const int q1[4],
+                                                 uint64_t &idx_out)
+{
+    int best[16], bi[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            v |= (uint32_t)(((64 - kW16[i]) * q0[c] + kW16[i] * q1[c] + 32) >> 6) << (8 * c);
+        const int sq = (int)__builtin_amdgcn_udot4(v, v, 0u, false);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int d = sq - 2 * (int)__builtin_amdgcn_udot4(v, px[k], 0u, false);
+            if (i == 0 || d < best[k]) {
+                best[k] = d;
+                bi[k] = i;
+            }
+        }
+    }
+    uint32_t sse = 0;
+    uint64_t ix = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        sse += (uint32_t)(best[k] + (int)__builtin_amdgcn_udot4(px[k], px[k], 0u, false));
+        ix |= (uint64_t)bi[k] << (4 * k);
+    }
+    idx_out = ix;
+    return sse;
+}
+
+// stage 0 itself; k_quant_probe6 has stored the first projection's indices
+// (qidx slot 208) for the blocks it may take
+__global__ void __launch_bounds__(256) k_fit6(Params p, Workspace ws, uint4 *__restrict__ dst,
+                                              double *__restrict__ err_out)
+{
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= p.n) return;
+    const BlockMeta meta = ws.meta[b];
+    if ((meta.flags & 7u) != 2u || !((meta.pvalid >> 6) & 1u)) return;   // integral, supported, not final, mode 6 legal
+    uint32_t px[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) px[i] = ws.px[(size_t)b * 16 + i];
+    uint64_t idx = ws.qidx[(size_t)b * kQuantTasks + 208];
+    uint32_t best = 0xffffffffu;
+    uint64_t bidx = 0;
+    int b0[4] = {0, 0, 0, 0}, b1[4] = {0, 0, 0, 0};
+#pragma unroll 1
+    for (int it = 0; it < 2; ++it) {
+        // least squares over the texels: x ~ ((64 - w) e0 + w e1) / 64
+        int a00 = 0, a01 = 0, a11 = 0, r0[4] = {0, 0, 0, 0}, r1[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int w = kW16[(idx >> (4 * k)) & 15u], u = 64 - w;
+            a00 += u * u;
+            a01 += u * w;
+            a11 += w * w;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int x = (int)((px[k] >> (8 * c)) & 255u);
+                r0[c] += u * x;
+                r1[c] += w * x;
+            }
+        }
+        const long long det = (long long)a00 * a11 - (long long)a01 * a01;
+        double e0[4], e1[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (det == 0) {
+                int sum = 0;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) sum += (int)((px[k] >> (8 * c)) & 255u);
+                e0[c] = e1[c] = (double)sum / 16.0;
+            } else {
+                e0[c] = (64.0 * (double)((long long)a11 * r0[c] - (long long)a01 * r1[c])) / (double)det;
+                e1[c] = (64.0 * (double)((long long)a00 * r1[c] - (long long)a01 * r0[c])) / (double)det;
+            }
+            e0[c] = e0[c] < 0.0 ? 0.0 : (e0[c] > 255.0 ? 255.0 : e0[c]);
+            e1[c] = e1[c] < 0.0 ? 0.0 : (e1[c] > 255.0 ? 255.0 : e1[c]);
+        }
+        uint32_t cbest = 0xffffffffu;
+        uint64_t cidx = 0;
+        int c0[4] = {0, 0, 0, 0}, c1[4] = {0, 0, 0, 0};
+#pragma unroll 1
+        for (int pp = 0; pp < 4; ++pp) {
+            const int p0 = pp >> 1, p1 = pp & 1;
+            int q0[4], q1[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                int v0 = (int)floor((e0[c] - (double)p0) * 0.5 + 0.5), v1 = (int)floor((e1[c] - (double)p1) * 0.5 + 0.5);
+                v0 = v0 < 0 ? 0 : (v0 > 127 ? 127 : v0);
+                v1 = v1 < 0 ? 0 : (v1 > 127 ? 127 : v1);
+                q0[c] = 2 * v0 + p0;
+                q1[c] = 2 * v1 + p1;
+            }
+            uint64_t ti;
+            const uint32_t sse = fit6_palette(px, q0, q1, ti);
+            if (sse < cbest) {
+                cbest = sse;
+                cidx = ti;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    c0[c] = q0[c];
+                    c1[c] = q1[c];
+                }
+            }
+        }
+        if (cbest < best) {
+            best = cbest;
+            bidx = cidx;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                b0[c] = c0[c];
+                b1[c] = c1[c];
+            }
+        }
+        idx = cidx;
+    }
+    uint8_t ep[3][2][4] = {};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        ep[0][0][c] = (uint8_t)b0[c];
+        ep[0][1][c] = (uint8_t)b1[c];
+    }
+    // integral texels: the palette error is the decoded block's error (the
+    // oracle model checks the two agree, tests/test_gpu_bc7_sample.py)
+    const double d = (double)best;
+    if (!(d <= p.bound_sse)) return;
+    uint32_t w[4];
+    pack_single(6, 0, ep, bidx, w);
+    const uint32_t o = out_block(p, b);
+    dst[o] = make_uint4(w[0], w[1], w[2], w[3]);
+    if (err_out) err_out[o] = d;
+    ws.meta[b].flags = meta.flags | 4u;
+}
+
 // K1t (performance < 1): optQuantTrace_d for the partitions of the single-index
 // modes with at most 8 clusters (0-3, 7) of blocks whose range exceeds
 // 255 * performance (CompressSingleIndexBlock :606-633); overwrites what the
@@ -3297,8 +3450,8 @@ static void base_params(const gic_options &o, const DeviceState &st, double perf
 // H4 report of the calling thread's last BC7 call (gic_last_h4_report)
 thread_local uint32_t t_h4_rerun = 0, t_h4_nonterm = 0;
 // blocks entering each stage of the calling thread's last BC7 call
-// (gic_last_bc7_stages): bounded exit = probe 6, probe 3, probe 1, search
-thread_local uint32_t t_stage_in[4] = {0, 0, 0, 0};
+// (gic_last_bc7_stages): bounded exit = mode-6 fit, probe 6, probe 3, probe 1, search
+thread_local uint32_t t_stage_in[5] = {0, 0, 0, 0, 0};
 thread_local int t_nstages = 0;
 
 static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t total, const gic_options &o, void *dst,
@@ -3364,10 +3517,13 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
     // stage runs over that list in dense chunks.  The probes may use mode 6
     // on opaque blocks, which the reference's colour restriction leaves out
     // of its own search: any BC7 block within the bound meets the contract.
-    int stages[4], nstages = 0;
-    if (bounded)
+    // Stage 0 (-2, before the probes): the direct mode-6 fit (k_fit6).
+    int stages[5], nstages = 0;
+    if (bounded) {
+        if (valid_modes & 0x40u) stages[nstages++] = -2;
         for (int k : {0, 2, 3})
             if (valid_modes & (1u << order[k])) stages[nstages++] = k;
+    }
     stages[nstages++] = -1;   // the search itself
     // the search over one chunk (the modes in one launch sequence, or staged)
     auto search = [&](Params p, const Workspace &ws, hipStream_t s, bool integral) -> hipError_t {
@@ -3394,7 +3550,7 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
     const uint32_t *cur = nullptr;
     uint32_t cur_n = total;
     uint32_t ci = 0;
-    for (int k = 0; k < 4; ++k) t_stage_in[k] = 0;
+    for (int k = 0; k < 5; ++k) t_stage_in[k] = 0;
     t_nstages = nstages;
     for (int si = 0; si < nstages && cur_n; ++si) {
         const int pk = stages[si];
@@ -3412,7 +3568,16 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
                 hipLaunchKernelGGL(k_prep_image, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, *g, p, ws);
             else
                 hipLaunchKernelGGL(k_prep_f32, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, blocks, p, ws);
-            if (pk >= 0) {
+            if (pk == -2) {
+                Params pp = p;
+                pp.bound_sse = 64.0 * (double)o.bc7_mse_bound;
+                pp.probe = 1;
+                pp.stage_mask = 0x40u;
+                hipLaunchKernelGGL(k_quant_probe6, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, pp, ws);
+                hipLaunchKernelGGL(k_fit6, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, pp, ws, (uint4 *)dst, err);
+                hipLaunchKernelGGL(k_compact, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, pp, ws, out,
+                                   st->count + si);
+            } else if (pk >= 0) {
                 Params pp = p;
                 pp.att = host_attempts(pp, 2);
                 pp.decode_select = 1;
@@ -3578,9 +3743,9 @@ hipError_t bc7_nonterm(unsigned long long *n, int reset)
     return e;
 }
 
-void bc7_last_stages(uint32_t in[4], int *n)
+void bc7_last_stages(uint32_t in[5], int *n)
 {
-    for (int k = 0; k < 4; ++k) in[k] = bc7::t_stage_in[k];
+    for (int k = 0; k < 5; ++k) in[k] = bc7::t_stage_in[k];
     *n = bc7::t_nstages;
 }
 

@@ -2,12 +2,39 @@
 // (see gic_pipeline.h).
 #include "gic_pipeline.h"
 
+#include <sys/mman.h>
+#include <unistd.h>
+
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
 
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23   // Linux 5.14
+#endif
+
 namespace gic {
+
+void *alloc_image_data(size_t bytes)
+{
+    constexpr size_t kHuge = (size_t)2 << 20;
+    if (bytes < 2 * kHuge) return malloc(bytes ? bytes : 1);
+    void *p = nullptr;
+    if (posix_memalign(&p, kHuge, bytes) != 0) return nullptr;
+    (void)madvise(p, (bytes + kHuge - 1) & ~(kHuge - 1), MADV_HUGEPAGE);   // a hint: ignored where THP is off
+    return p;
+}
+
+// Faults in the pages of [p, p + bytes) for writing without touching their
+// contents (so it may run beside threads writing the same range); a no-op on
+// kernels without MADV_POPULATE_WRITE.
+static void populate_write(void *p, size_t bytes)
+{
+    static const uintptr_t page = (uintptr_t)sysconf(_SC_PAGESIZE);
+    const uintptr_t a = (uintptr_t)p & ~(page - 1), b = ((uintptr_t)p + bytes + page - 1) & ~(page - 1);
+    if (b > a) (void)madvise((void *)a, b - a, MADV_POPULATE_WRITE);
+}
 
 H2D h2d_mode()
 {
@@ -108,10 +135,11 @@ PiecePlan piece_plan(gic_format fmt, uint32_t blocks_x, uint64_t rows)
 {
     const uint64_t bx = blocks_x ? blocks_x : 1;
     auto clamp_rows = [](uint64_t r) { return r < 1 ? 1u : (r > 0xffffffffull ? 0xffffffffu : (uint32_t)r); };
-    const char *e = getenv("GIC_PIECE_BLOCKS");   // test / tuning hook
+    const char *e = getenv("GIC_PIECE_BLOCKS");   // test / tuning hooks
+    const char *f = getenv("GIC_PIECE_FIRST");
     if (e && atoll(e) > 0) {
         const uint32_t r = clamp_rows((uint64_t)atoll(e) / bx);
-        return PiecePlan{r, r};
+        return PiecePlan{f && atoll(f) > 0 ? clamp_rows((uint64_t)atoll(f) / bx) : r, r};
     }
     if (fmt == GIC_FMT_BC7) return PiecePlan{clamp_rows(rows / 16), 0xffffffffu};
     const uint32_t r = clamp_rows((1u << 18) / bx);
@@ -280,6 +308,14 @@ int run_pieces(Lane &lane, const EncodeArgs &a, const std::vector<Piece> &pieces
         uploaded.fail();   // wakes the encoder if it waits past the last posted piece
     });
 
+    // The caller's image pages are faulted in ahead of the copy-out stage, in
+    // piece order (a fresh allocation faults on first touch: several ms for an
+    // 8K BC1 image if the copies took them one by one).
+    std::thread populator([&] {
+        for (size_t k = 0; k < pieces.size() && !stop(); ++k)
+            if (pieces[k].h_out) populate_write(pieces[k].h_out, pieces[k].out_bytes);
+    });
+
     // Pieces with a host destination are encoded straight into pinned host
     // memory (the kernels' block stores cross PCIe as they retire), and the
     // download stage only copies each finished piece into the caller's image.
@@ -335,6 +371,7 @@ int run_pieces(Lane &lane, const EncodeArgs &a, const std::vector<Piece> &pieces
     if (rc != GIC_OK || e != hipSuccess) halt.store(true);   // the uploader stops at its next piece
     uploader.join();
     downloader.join();
+    populator.join();
     hipError_t ee = hipStreamSynchronize(lane.enc);
     if (e == hipSuccess) e = ee;
     ee = hipStreamSynchronize(lane.enc2);

@@ -112,6 +112,9 @@ int orc_bc6h_ev_p(void);
 /* bounded-exit probe model: mode 6 starts its shake from the quantiser's
  * first projection (thread-local switch; not the reference) */
 void orc_bc7_set_probe_init(int on);
+/* bounded-exit stage 0 model (gic_bc7.hip k_fit6): the direct mode-6 fit of one
+ * block; returns its palette's squared error */
+double orc_bc7_fit6(const float in[64], uint8_t out[16]);
 
 /* helpers exposed for unit tests */
 void orc_load_block_rgba8(const uint8_t *src, uint32_t width, uint32_t height,

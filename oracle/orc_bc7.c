@@ -1811,6 +1811,122 @@ double orc_bc7_block_ex(const float inN[64], uint8_t mode_mask, int src_has_alph
     return best;
 }
 
+/* Not the reference: the bounded exit's stage 0 (gic_bc7.hip k_fit6), the
+ * oracle model of the GPU's direct mode-6 fit.  From the quantiser's first
+ * projection (opt_quant_first, 16 clusters): least-squares endpoints for BC7's
+ * 4-bit weights (integer sums, the same f64 solve), each endpoint's 7-bit codes
+ * and parity bits chosen jointly by the palette error (texels to their nearest
+ * entry, first of least error), one refit from those indices, the better kept;
+ * packed as mode 6.  Returns the palette's squared error (= the decoded error
+ * for integral texels). */
+static const int kFitW16[16] = {0, 4, 9, 13, 17, 21, 26, 30, 34, 38, 43, 47, 51, 55, 60, 64};
+
+static unsigned fit6_palette(const int x[16][4], const int q0[4], const int q1[4], int idx[16])
+{
+    int pal[16][4];
+    for (int i = 0; i < 16; ++i)
+        for (int c = 0; c < 4; ++c) pal[i][c] = ((64 - kFitW16[i]) * q0[c] + kFitW16[i] * q1[c] + 32) >> 6;
+    unsigned sse = 0;
+    for (int k = 0; k < 16; ++k) {
+        int best = 0x7fffffff, bi = 0;
+        for (int i = 0; i < 16; ++i) {
+            int d = 0;
+            for (int c = 0; c < 4; ++c) d += (pal[i][c] - x[k][c]) * (pal[i][c] - x[k][c]);
+            if (d < best) {
+                best = d;
+                bi = i;
+            }
+        }
+        sse += (unsigned)best;
+        idx[k] = bi;
+    }
+    return sse;
+}
+
+double orc_bc7_fit6(const float inN[64], uint8_t out[16])
+{
+    pthread_once(&g_once, build_tables);
+    double in[16][4];
+    int x[16][4], idx[16];
+    for (int i = 0; i < 16; ++i)
+        for (int j = 0; j < 4; ++j) {
+            in[i][j] = inN[i * 4 + j] * 255.0f;
+            x[i][j] = (int)in[i][j];
+        }
+    opt_quant_first(in, 16, 16, idx, 4);
+    unsigned best = 0xffffffffu;
+    int bidx[16], b0[4] = {0, 0, 0, 0}, b1[4] = {0, 0, 0, 0};
+    for (int it = 0; it < 2; ++it) {
+        int a00 = 0, a01 = 0, a11 = 0, r0[4] = {0, 0, 0, 0}, r1[4] = {0, 0, 0, 0};
+        for (int k = 0; k < 16; ++k) {
+            const int w = kFitW16[idx[k]], u = 64 - w;
+            a00 += u * u;
+            a01 += u * w;
+            a11 += w * w;
+            for (int c = 0; c < 4; ++c) {
+                r0[c] += u * x[k][c];
+                r1[c] += w * x[k][c];
+            }
+        }
+        const long long det = (long long)a00 * a11 - (long long)a01 * a01;
+        double e0[4], e1[4];
+        for (int c = 0; c < 4; ++c) {
+            if (det == 0) {
+                int sum = 0;
+                for (int k = 0; k < 16; ++k) sum += x[k][c];
+                e0[c] = e1[c] = (double)sum / 16.0;
+            } else {
+                e0[c] = (64.0 * (double)((long long)a11 * r0[c] - (long long)a01 * r1[c])) / (double)det;
+                e1[c] = (64.0 * (double)((long long)a00 * r1[c] - (long long)a01 * r0[c])) / (double)det;
+            }
+            e0[c] = e0[c] < 0.0 ? 0.0 : (e0[c] > 255.0 ? 255.0 : e0[c]);
+            e1[c] = e1[c] < 0.0 ? 0.0 : (e1[c] > 255.0 ? 255.0 : e1[c]);
+        }
+        unsigned cbest = 0xffffffffu;
+        int cidx[16], c0[4] = {0, 0, 0, 0}, c1[4] = {0, 0, 0, 0};
+        for (int pp = 0; pp < 4; ++pp) {
+            const int p0 = pp >> 1, p1 = pp & 1;
+            int q0[4], q1[4], ti[16];
+            for (int c = 0; c < 4; ++c) {
+                int v0 = (int)floor((e0[c] - (double)p0) * 0.5 + 0.5), v1 = (int)floor((e1[c] - (double)p1) * 0.5 + 0.5);
+                v0 = v0 < 0 ? 0 : (v0 > 127 ? 127 : v0);
+                v1 = v1 < 0 ? 0 : (v1 > 127 ? 127 : v1);
+                q0[c] = 2 * v0 + p0;
+                q1[c] = 2 * v1 + p1;
+            }
+            const unsigned sse = fit6_palette(x, q0, q1, ti);
+            if (sse < cbest) {
+                cbest = sse;
+                memcpy(cidx, ti, sizeof(ti));
+                memcpy(c0, q0, sizeof(q0));
+                memcpy(c1, q1, sizeof(q1));
+            }
+        }
+        if (cbest < best) {
+            best = cbest;
+            memcpy(bidx, cidx, sizeof(cidx));
+            memcpy(b0, c0, sizeof(c0));
+            memcpy(b1, c1, sizeof(c1));
+        }
+        memcpy(idx, cidx, sizeof(cidx));
+    }
+    bc7_enc e;
+    memset(&e, 0, sizeof(e));
+    mode_setup(&e, 6);
+    unsigned colour[3][2] = {{0, 0}, {0, 0}, {0, 0}};
+    int idx3[3][16];
+    for (int k = 0; k < 2; ++k) {
+        const int *q = k ? b1 : b0;
+        unsigned wd = (unsigned)(q[0] & 1);
+        for (int c = 0; c < 4; ++c) wd |= (unsigned)(q[c] >> 1) << (1 + 7 * c);
+        colour[0][k] = wd;
+    }
+    memcpy(idx3[0], bidx, sizeof(bidx));
+    memset(out, 0, 16);
+    pack_single(&e, 6, 0, colour, idx3, out);
+    return (double)best;
+}
+
 /* ----------------------------------------------------------- decoder --- */
 /* Standard BC7 decode (format spec) for tolerance checks. */
 static unsigned get_bits(const uint8_t *b, int *pos, int n)

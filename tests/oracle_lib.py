@@ -78,6 +78,8 @@ def lib() -> ctypes.CDLL:
         _lib.orc_encode_image_bc7enc_rows.restype = ctypes.c_int
         _lib.orc_bc7_set_probe_init.argtypes = [ctypes.c_int]
         _lib.orc_bc7_set_probe_init.restype = None
+        _lib.orc_bc7_fit6.argtypes = [vp, vp]
+        _lib.orc_bc7_fit6.restype = ctypes.c_double
         _lib.orc_encode_bc6h_blocks.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp]
         _lib.orc_encode_bc6h_blocks.restype = ctypes.c_int
         _lib.orc_bc6h_block.argtypes = [vp, ctypes.c_int, vp]
@@ -200,6 +202,18 @@ def bc7_blocks_ex(blocks: np.ndarray, mode_mask: int = 0xFF, colour_restrict: bo
         lib().orc_bc7_block_ex(f.ctypes.data, mode_mask, int(has_alpha), 1.0, int(colour_restrict), 1, 1.0,
                                shake_ranks, out[k].ctypes.data)
     return out
+
+
+def bc7_fit6_blocks(blocks: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    """orc_bc7_fit6 (the bounded exit's direct mode-6 fit, gic_bc7.hip k_fit6)
+    over (n, 16, 4) uint8 blocks: (packed blocks, palette squared errors)."""
+    b = np.ascontiguousarray(blocks, dtype=np.uint8).reshape(-1, 64)
+    out = np.zeros((b.shape[0], 16), np.uint8)
+    err = np.zeros(b.shape[0])
+    for k in range(b.shape[0]):
+        f = (b[k].astype(np.float32) / np.float32(255.0)).astype(np.float32)
+        err[k] = lib().orc_bc7_fit6(f.ctypes.data, out[k].ctypes.data)
+    return out, err
 
 
 def encode_image_bc7enc(img: np.ndarray, fast: bool = False, perceptual: bool = True) -> np.ndarray:

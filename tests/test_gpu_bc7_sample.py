@@ -167,11 +167,11 @@ def _mode_of(blocks):
 
 
 def test_bc7_bounded_matches_model(gpu):
-    """The bounded path, block by block, is: the oracle's mode-6 search (no
+    """The bounded path, block by block, is: the oracle's direct mode-6 fit
+    (orc_bc7_fit6) if that decodes within the bound, else its mode-6 search (no
     colour restriction; its shaker started from the quantiser's first
-    projection, the probe's shortcut) if that decodes within the bound, else
-    its mode-3 search with 2 partitions shaken likewise, else mode 1, else the
-    exact search."""
+    projection, the probe's shortcut) if that does, else its mode-3 search with
+    2 partitions shaken likewise, else mode 1, else the exact search."""
     import torch
     g1 = synth.g1(8192, 8192)   # the bench texture: most blocks end in the probe
     mixed = np.ascontiguousarray(np.concatenate([g1[2048:2064, 512:640], synth.g1(128, 16, seed=5)], axis=1))
@@ -187,7 +187,11 @@ def test_bc7_bounded_matches_model(gpu):
         got = dst.cpu().numpy().reshape(-1, 16)
         sb = _src_blocks(img)
         model = oracle_lib.encode_image_bc7(img)
-        done = np.zeros(nb, bool)
+        fit, fit_err = oracle_lib.bc7_fit6_blocks(sb)
+        done = _block_mse(fit, sb) <= MSE_ABS
+        assert np.array_equal(_block_mse(fit, sb) * 64.0, fit_err)   # the palette error is the decoded error
+        model[done] = fit[done]
+        fit_share = done.mean()
         for mode in (6, 3, 1):
             # the mode-6 probe starts its shaker from the quantiser's first projection (k_quant_probe6)
             oracle_lib.lib().orc_bc7_set_probe_init(int(mode == 6))
@@ -198,7 +202,8 @@ def test_bc7_bounded_matches_model(gpu):
             ok = ~done & (_mode_of(cand) == mode) & (_block_mse(cand, sb) <= MSE_ABS)
             model[ok] = cand[ok]
             done |= ok
-        print(f"\n{w}x{h}: {100 * done.mean():.1f}% of blocks final after the probe")
+        print(f"\n{w}x{h}: {100 * fit_share:.1f}% of blocks final after the mode-6 fit, "
+              f"{100 * done.mean():.1f}% after the probes")
         assert np.array_equal(got, model), _mismatch_report(got, model)
 
 

@@ -6,6 +6,7 @@ search.
     python tools/time_bc7_bounded.py [--rows 256] [--bound 0.5] [--shake-ranks 0]
 """
 import argparse
+import hashlib
 import os
 import sys
 
@@ -41,7 +42,8 @@ def main():
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1)
     print(f"bound {a.bound} shake_ranks {a.shake_ranks}: {rows} block rows in {ms:.1f} ms = "
-          f"{size * rows * 4 / ms / 1e3:.2f} Mpix/s", flush=True)
+          f"{size * rows * 4 / ms / 1e3:.2f} Mpix/s, output sha1 {hashlib.sha1(dst.cpu().numpy().tobytes()).hexdigest()[:16]}",
+          flush=True)
 
 
 if __name__ == "__main__":
