@@ -65,6 +65,44 @@ def main():
         print(f"{a.pieces} pieces, blocks to {name}: {best:.3f} ms", flush=True)
     torch.cuda.synchronize()
     print("identical:", bool(torch.equal(dev_dst.cpu(), host_dst)))
+    # the pipeline's shape without its threads: piece k's rows uploaded (pinned
+    # source, one stream) into the buffer the kernels read, its encode waiting on
+    # that upload's event; then the same with the whole source resident
+    host_src = src.cpu().pin_memory()
+    slab = torch.empty_like(src)
+    row_bytes = size * 4 * 4 * rows
+    flat_h, flat_d = host_src.view(-1), slab.view(-1)
+    for name, wait in (("piecewise upload + encode (event per piece)", True), ("resident, same launches", False)):
+        best = 1e9
+        for _ in range(a.reps):
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(streams[0])
+            streams[1].wait_stream(streams[0])
+            up_stream.wait_stream(streams[0])
+            evs = []
+            for k in range(a.pieces):
+                if wait:
+                    with torch.cuda.stream(up_stream):
+                        flat_d[k * row_bytes:(k + 1) * row_bytes].copy_(flat_h[k * row_bytes:(k + 1) * row_bytes],
+                                                                        non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(up_stream)
+                    evs.append(ev)
+            for k in range(a.pieces):
+                s = streams[k % 2]
+                if wait:
+                    s.wait_event(evs[k])
+                rc = lib.gic_hip_encode_rows(1, slab.data_ptr() if wait else src.data_ptr(), size, size, 1, 4,
+                                             size * 4, k * rows, rows, ctypes.byref(opts),
+                                             host_dst.data_ptr() + k * rows * 2048 * 8, None,
+                                             ctypes.c_void_p(s.cuda_stream))
+                assert rc == 0, rc
+            streams[0].wait_stream(streams[1])
+            e1.record(streams[0])
+            torch.cuda.synchronize()
+            best = min(best, e0.elapsed_time(e1))
+        print(f"{a.pieces} pieces, {name}: {best:.3f} ms", flush=True)
 
 
 if __name__ == "__main__":
