@@ -1719,10 +1719,9 @@ __global__ void __launch_bounds__(256) k_quant_probe6(Params p, Workspace ws)
 
 // Bounded exit, stage 0 (round 6; not the reference's search): a mode-6 block
 // straight from the quantiser's first projection -- least-squares endpoints for
-// BC7's 4-bit interpolation weights, both endpoints' 7-bit codes and parity
-// bits chosen jointly by the error of the resulting palette (every texel taken
-// to its nearest entry), then one refit from those indices, the better of the
-// two kept.  Final when the packed block decodes within the bound, like a probe:
+// BC7's 4-bit interpolation weights, each endpoint's 7-bit codes and parity bit
+// the nearest to them, every texel taken to its nearest palette entry, then one
+// refit from those indices, the better of the two kept.  Final when the packed block decodes within the bound, like a probe:
 // it only decides which blocks skip the later stages, and a final block meets
 // the contract by the bound.  Modelled bit for bit by oracle/orc_bc7.c
 // orc_bc7_fit6 (integer sums, the same f64 solve and rounding).  On 8K G1 it
@@ -1739,6 +1738,11 @@ __device__ __forceinline__ uint32_t fit6_palette(const uint32_t px[16], const in
 {
     int best[16], bi[16];
 #pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        best[k] = 0x7fffffff;
+        bi[k] = 0;
+    }
+#pragma unroll 1
     for (int i = 0; i < 16; ++i) {
         uint32_t v = 0;
 #pragma unroll
@@ -1748,7 +1752,7 @@ __device__ __forceinline__ uint32_t fit6_palette(const uint32_t px[16], const in
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const int d = sq - 2 * (int)__builtin_amdgcn_udot4(v, px[k], 0u, false);
-            if (i == 0 || d < best[k]) {
+            if (d < best[k]) {
                 best[k] = d;
                 bi[k] = i;
             }
@@ -1763,6 +1767,43 @@ __device__ __forceinline__ uint32_t fit6_palette(const uint32_t px[16], const in
     }
     idx_out = ix;
     return sse;
+}
+
+// EncodeSingleIndexBlock's layout for mode 6 (pack_single's, specialised:
+// every field at a fixed bit position): mode bit 6, R0 R1 G0 G1 B0 B1 A0 A1 as
+// 7-bit codes, the two parity bits, texel 0's index in 3 bits (anchor: a set
+// top bit swaps the endpoints and inverts every index), the others in 4
+__device__ __forceinline__ void pack_mode6(const int q0_in[4], const int q1_in[4], uint64_t idx, uint32_t w[4])
+{
+    const bool flip = (idx & 8u) != 0;
+    int q0[4], q1[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        q0[c] = flip ? q1_in[c] : q0_in[c];
+        q1[c] = flip ? q0_in[c] : q1_in[c];
+    }
+    if (flip) idx = ~idx;   // 15 - i in every nibble
+    uint64_t lo = 1u << 6, hi = 0;
+    int pos = 7;
+    auto put = [&](uint64_t v, int n) {
+        if (pos < 64) lo |= v << pos;
+        if (pos + n > 64) hi |= pos >= 64 ? v << (pos - 64) : v >> (64 - pos);
+        pos += n;
+    };
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        put((uint64_t)(q0[c] >> 1), 7);
+        put((uint64_t)(q1[c] >> 1), 7);
+    }
+    put((uint64_t)(q0[0] & 1), 1);
+    put((uint64_t)(q1[0] & 1), 1);
+    put(idx & 7u, 3);
+#pragma unroll
+    for (int k = 1; k < 16; ++k) put((idx >> (4 * k)) & 15u, 4);
+    w[0] = (uint32_t)lo;
+    w[1] = (uint32_t)(lo >> 32);
+    w[2] = (uint32_t)hi;
+    w[3] = (uint32_t)(hi >> 32);
 }
 
 // stage 0 itself; k_quant_probe6 has stored the first projection's indices
@@ -1783,6 +1824,9 @@ __global__ void __launch_bounds__(256) k_fit6(Params p, Workspace ws, uint4 *__r
     int b0[4] = {0, 0, 0, 0}, b1[4] = {0, 0, 0, 0};
 #pragma unroll 1
     for (int it = 0; it < 2; ++it) {
+        // (opaque: otherwise the 64 channel values are hoisted out of the loop)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(px[k]));
         // least squares over the texels: x ~ ((64 - w) e0 + w e1) / 64
         int a00 = 0, a01 = 0, a11 = 0, r0[4] = {0, 0, 0, 0}, r1[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -1814,33 +1858,30 @@ __global__ void __launch_bounds__(256) k_fit6(Params p, Workspace ws, uint4 *__r
             e0[c] = e0[c] < 0.0 ? 0.0 : (e0[c] > 255.0 ? 255.0 : e0[c]);
             e1[c] = e1[c] < 0.0 ? 0.0 : (e1[c] > 255.0 ? 255.0 : e1[c]);
         }
-        uint32_t cbest = 0xffffffffu;
-        uint64_t cidx = 0;
-        int c0[4] = {0, 0, 0, 0}, c1[4] = {0, 0, 0, 0};
-#pragma unroll 1
-        for (int pp = 0; pp < 4; ++pp) {
-            const int p0 = pp >> 1, p1 = pp & 1;
-            int q0[4], q1[4];
+        // each endpoint's parity: the one whose 7-bit codes land nearer its
+        // least-squares values (parity 0 on a tie)
+        int c0[4], c1[4];
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                int v0 = (int)floor((e0[c] - (double)p0) * 0.5 + 0.5), v1 = (int)floor((e1[c] - (double)p1) * 0.5 + 0.5);
-                v0 = v0 < 0 ? 0 : (v0 > 127 ? 127 : v0);
-                v1 = v1 < 0 ? 0 : (v1 > 127 ? 127 : v1);
-                q0[c] = 2 * v0 + p0;
-                q1[c] = 2 * v1 + p1;
-            }
-            uint64_t ti;
-            const uint32_t sse = fit6_palette(px, q0, q1, ti);
-            if (sse < cbest) {
-                cbest = sse;
-                cidx = ti;
+        for (int i = 0; i < 2; ++i) {
+            const double *e = i ? e1 : e0;
+            int q[2][4];
+            double qe[2] = {0.0, 0.0};
+#pragma unroll
+            for (int par = 0; par < 2; ++par)
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    c0[c] = q0[c];
-                    c1[c] = q1[c];
+                    int v = (int)floor((e[c] - (double)par) * 0.5 + 0.5);
+                    v = v < 0 ? 0 : (v > 127 ? 127 : v);
+                    q[par][c] = 2 * v + par;
+                    const double d = (double)q[par][c] - e[c];
+                    qe[par] += d * d;
                 }
-            }
+            const int pb = qe[1] < qe[0] ? 1 : 0;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) (i ? c1 : c0)[c] = q[pb][c];
         }
+        uint64_t cidx;
+        const uint32_t cbest = fit6_palette(px, c0, c1, cidx);
         if (cbest < best) {
             best = cbest;
             bidx = cidx;
@@ -1852,18 +1893,12 @@ __global__ void __launch_bounds__(256) k_fit6(Params p, Workspace ws, uint4 *__r
         }
         idx = cidx;
     }
-    uint8_t ep[3][2][4] = {};
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        ep[0][0][c] = (uint8_t)b0[c];
-        ep[0][1][c] = (uint8_t)b1[c];
-    }
     // integral texels: the palette error is the decoded block's error (the
     // oracle model checks the two agree, tests/test_gpu_bc7_sample.py)
     const double d = (double)best;
     if (!(d <= p.bound_sse)) return;
     uint32_t w[4];
-    pack_single(6, 0, ep, bidx, w);
+    pack_mode6(b0, b1, bidx, w);
     const uint32_t o = out_block(p, b);
     dst[o] = make_uint4(w[0], w[1], w[2], w[3]);
     if (err_out) err_out[o] = d;
@@ -2863,6 +2898,22 @@ __global__ void __launch_bounds__(256) k_compact(Params p, Workspace ws, uint32_
     if (keep) out[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = out_block(p, b);
 }
 
+// A stage skipped for the rest of its chunks (run_chunks: its first chunk
+// finished under 1 % of its blocks): every block of the chunk goes on to the
+// next stage's list as it is (k_compact's append, every block kept).
+__global__ void __launch_bounds__(256) k_pass_on(Params p, uint32_t *__restrict__ out, uint32_t *__restrict__ count)
+{
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t m = __ballot(b < p.n);
+    if (!m) return;
+    const int lane = (int)__lane_id();
+    const int leader = __builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, leader);
+    if (b < p.n) out[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = out_block(p, b);
+}
+
 // ----------------------------------------------------------------- host ---
 
 static void build_sp_table(std::vector<SpEntry> &tab)
@@ -3552,11 +3603,19 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
     uint32_t ci = 0;
     for (int k = 0; k < 5; ++k) t_stage_in[k] = 0;
     t_nstages = nstages;
+    // A probe stage (stage 0 included) whose first chunk finishes under 1 % of
+    // its blocks is skipped for the rest of the call: its remaining chunks go
+    // on to the next stage untouched (k_pass_on).  On content no probe suits
+    // (G2: independent channel noise, 0 % within the bound) the bounded exit
+    // then costs what the search does, plus one chunk per probe; which blocks a
+    // skipped chunk would have finished only changes which contract-meeting
+    // block they get (the search's own).
     for (int si = 0; si < nstages && cur_n; ++si) {
         const int pk = stages[si];
         t_stage_in[si] = cur_n;
         const bool last_stage = si == nstages - 1;
         uint32_t *out = bounded ? st->list[si & 1] : nullptr;
+        bool skip_rest = false;
         for (uint32_t first = 0; first < cur_n; first += chunk, ++ci) {
             const Workspace &ws = st->ws[ci % (uint32_t)nsets];
             s = st->lane[ci % (uint32_t)nsets];
@@ -3564,6 +3623,20 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
             p.first = first;
             p.n = (cur_n - first) < chunk ? (cur_n - first) : chunk;
             p.list = cur ? cur + first : nullptr;
+            if (!last_stage && first == chunk && cur_n > 2 * chunk) {
+                // the first chunk's survivors: its lane is drained for the count
+                e = hipStreamSynchronize(st->lane[(ci - 1) % (uint32_t)nsets]);
+                uint32_t kept = 0;
+                if (e == hipSuccess) e = hipMemcpy(&kept, st->count + si, sizeof(uint32_t), hipMemcpyDeviceToHost);
+                if (e != hipSuccess) return e;
+                skip_rest = (uint64_t)(chunk - kept) * 100u < (uint64_t)chunk;
+            }
+            if (skip_rest) {
+                hipLaunchKernelGGL(k_pass_on, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, p, out, st->count + si);
+                e = hipGetLastError();
+                if (e != hipSuccess) return e;
+                continue;
+            }
             if (g)
                 hipLaunchKernelGGL(k_prep_image, dim3((p.n + wg - 1) / wg), dim3(wg), 0, s, *g, p, ws);
             else

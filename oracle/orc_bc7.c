@@ -1815,8 +1815,9 @@ double orc_bc7_block_ex(const float inN[64], uint8_t mode_mask, int src_has_alph
  * oracle model of the GPU's direct mode-6 fit.  From the quantiser's first
  * projection (opt_quant_first, 16 clusters): least-squares endpoints for BC7's
  * 4-bit weights (integer sums, the same f64 solve), each endpoint's 7-bit codes
- * and parity bits chosen jointly by the palette error (texels to their nearest
- * entry, first of least error), one refit from those indices, the better kept;
+ * and parity bit the nearest to them (parity 0 on a tie), texels to their
+ * nearest palette entry (first of least error), one refit from those indices,
+ * the better kept;
  * packed as mode 6.  Returns the palette's squared error (= the decoded error
  * for integral texels). */
 static const int kFitW16[16] = {0, 4, 9, 13, 17, 21, 26, 30, 34, 38, 43, 47, 51, 55, 60, 64};
@@ -1882,26 +1883,23 @@ double orc_bc7_fit6(const float inN[64], uint8_t out[16])
             e0[c] = e0[c] < 0.0 ? 0.0 : (e0[c] > 255.0 ? 255.0 : e0[c]);
             e1[c] = e1[c] < 0.0 ? 0.0 : (e1[c] > 255.0 ? 255.0 : e1[c]);
         }
-        unsigned cbest = 0xffffffffu;
-        int cidx[16], c0[4] = {0, 0, 0, 0}, c1[4] = {0, 0, 0, 0};
-        for (int pp = 0; pp < 4; ++pp) {
-            const int p0 = pp >> 1, p1 = pp & 1;
-            int q0[4], q1[4], ti[16];
-            for (int c = 0; c < 4; ++c) {
-                int v0 = (int)floor((e0[c] - (double)p0) * 0.5 + 0.5), v1 = (int)floor((e1[c] - (double)p1) * 0.5 + 0.5);
-                v0 = v0 < 0 ? 0 : (v0 > 127 ? 127 : v0);
-                v1 = v1 < 0 ? 0 : (v1 > 127 ? 127 : v1);
-                q0[c] = 2 * v0 + p0;
-                q1[c] = 2 * v1 + p1;
-            }
-            const unsigned sse = fit6_palette(x, q0, q1, ti);
-            if (sse < cbest) {
-                cbest = sse;
-                memcpy(cidx, ti, sizeof(ti));
-                memcpy(c0, q0, sizeof(q0));
-                memcpy(c1, q1, sizeof(q1));
-            }
+        int c0[4], c1[4], cidx[16];
+        for (int i = 0; i < 2; ++i) {
+            const double *e = i ? e1 : e0;
+            int q[2][4];
+            double qe[2] = {0.0, 0.0};
+            for (int par = 0; par < 2; ++par)
+                for (int c = 0; c < 4; ++c) {
+                    int v = (int)floor((e[c] - (double)par) * 0.5 + 0.5);
+                    v = v < 0 ? 0 : (v > 127 ? 127 : v);
+                    q[par][c] = 2 * v + par;
+                    const double d = (double)q[par][c] - e[c];
+                    qe[par] += d * d;
+                }
+            const int pb = qe[1] < qe[0] ? 1 : 0;
+            memcpy(i ? c1 : c0, q[pb], sizeof(q[pb]));
         }
+        const unsigned cbest = fit6_palette(x, c0, c1, cidx);
         if (cbest < best) {
             best = cbest;
             memcpy(bidx, cidx, sizeof(cidx));
