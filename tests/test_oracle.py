@@ -145,3 +145,25 @@ def test_bc6h_oracle_blocks_are_valid():
     ok = (two_bit < 2) | np.isin(five_bit, [0x02, 0x06, 0x0a, 0x0e, 0x12, 0x16, 0x1a, 0x1e])
     assert ok.all()
     assert np.isfinite(err).all()
+
+
+def test_bc7_fit6_model():
+    """The bounded exit's stage-0 model (orc_bc7_fit6, gic_bc7.hip k_fit6): every
+    block is a mode-6 block whose decode error is the returned palette error,
+    the G0 gradient is always within MSE 0.5, G1 (grey-axis noise) mostly, and
+    random RGBA never."""
+    def blocks(img):
+        h, w, _ = img.shape
+        return img.reshape(h // 4, 4, w // 4, 4, 4).transpose(0, 2, 1, 3, 4).reshape(-1, 16, 4)
+
+    for img, lo, hi in ((synth.g0(8192, 8192)[4096:4112, :1024], 1.0, 1.0),
+                        (synth.g1(8192, 2048)[1024:1040, 2048:3072], 0.9, 1.0),
+                        (np.random.default_rng(3).integers(0, 256, (16, 256, 4), dtype=np.uint8), 0.0, 0.0)):
+        sb = blocks(np.ascontiguousarray(img))
+        out, err = oracle_lib.bc7_fit6_blocks(sb)
+        assert all((b[0] & 0x7f) == 64 for b in out)   # mode 6
+        dec = oracle_lib.bc7_decode(out).astype(np.float64)
+        sse = ((dec - sb.astype(np.float64)) ** 2).sum(axis=(1, 2))
+        assert np.array_equal(sse, err)
+        share = (sse <= 32.0).mean()
+        assert lo <= share <= hi, share
