@@ -321,8 +321,9 @@ def _host_header(lib, a):
 def last_bc7_stages() -> list[int]:
     """Blocks entering each stage of this thread's last BC7 call
     (gic_last_bc7_stages): [all, after the direct mode-6 fit, after the mode-6
-    probe, after mode 3, after mode 1] with the bounded exit, [all] without."""
-    arr, n = (ctypes.c_uint32 * 5)(), ctypes.c_int(0)
+    probe, after mode 3, after mode 1, after mode 4] with the bounded exit, [all]
+    without."""
+    arr, n = (ctypes.c_uint32 * 6)(), ctypes.c_int(0)
     _check(library().gic_last_bc7_stages(arr, ctypes.byref(n)))
     return [int(arr[k]) for k in range(n.value)]
 

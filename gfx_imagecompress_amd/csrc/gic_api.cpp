@@ -56,7 +56,7 @@ hipError_t bc6h_iter_cap(int cap, unsigned long long *hits, int reset);
 hipError_t bc7_nonterm(unsigned long long *n, int reset);
 hipError_t bc6h_nonterm(unsigned long long *n, int reset);
 void bc7_last_h4(uint32_t *rerun, uint32_t *nonterm);
-void bc7_last_stages(uint32_t in[5], int *n);
+void bc7_last_stages(uint32_t in[6], int *n);
 }  // namespace gic
 
 static bool is_bc6h(gic_format f) { return f == GIC_FMT_BC6H || f == GIC_FMT_BC6H_SF; }
@@ -74,7 +74,7 @@ static int hip_fail(hipError_t e)
 
 extern "C" int gic_last_hip_error(void) { return t_last_hip_error; }
 
-extern "C" int gic_last_bc7_stages(uint32_t blocks_in[5], int *stages)
+extern "C" int gic_last_bc7_stages(uint32_t blocks_in[6], int *stages)
 {
     if (!blocks_in || !stages) return GIC_EINVAL;
     gic::bc7_last_stages(blocks_in, stages);

@@ -3178,7 +3178,7 @@ static hipError_t get_lists(DeviceState &st, uint32_t total)
 {
     hipError_t e = hipSuccess;
     if (!st.count) {
-        e = hipMalloc(&st.count, 4 * sizeof(uint32_t));
+        e = hipMalloc(&st.count, 8 * sizeof(uint32_t));   // one survivor counter per stage
         if (e != hipSuccess) return e;
     }
     if (st.list_cap >= total) return hipSuccess;
@@ -3501,8 +3501,8 @@ static void base_params(const gic_options &o, const DeviceState &st, double perf
 // H4 report of the calling thread's last BC7 call (gic_last_h4_report)
 thread_local uint32_t t_h4_rerun = 0, t_h4_nonterm = 0;
 // blocks entering each stage of the calling thread's last BC7 call
-// (gic_last_bc7_stages): bounded exit = mode-6 fit, probe 6, probe 3, probe 1, search
-thread_local uint32_t t_stage_in[5] = {0, 0, 0, 0, 0};
+// (gic_last_bc7_stages): bounded exit = mode-6 fit, probes 6, 3, 1 and 4, search
+thread_local uint32_t t_stage_in[6] = {0, 0, 0, 0, 0, 0};
 thread_local int t_nstages = 0;
 
 static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t total, const gic_options &o, void *dst,
@@ -3551,7 +3551,7 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
     if (bounded) {
         e = get_lists(*st, total);
         if (e != hipSuccess) return e;
-        e = hipMemsetAsync(st->count, 0, 4 * sizeof(uint32_t), s);
+        e = hipMemsetAsync(st->count, 0, 8 * sizeof(uint32_t), s);
         if (e != hipSuccess) return e;
     }
     e = hipEventRecord(st->ev_fork, s);   // fork: the lanes start after the caller's prior work
@@ -3569,10 +3569,10 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
     // on opaque blocks, which the reference's colour restriction leaves out
     // of its own search: any BC7 block within the bound meets the contract.
     // Stage 0 (-2, before the probes): the direct mode-6 fit (k_fit6).
-    int stages[5], nstages = 0;
+    int stages[6], nstages = 0;
     if (bounded) {
         if (valid_modes & 0x40u) stages[nstages++] = -2;
-        for (int k : {0, 2, 3})
+        for (int k : {0, 2, 3, 1})   // modes 6, 3, 1, then 4
             if (valid_modes & (1u << order[k])) stages[nstages++] = k;
     }
     stages[nstages++] = -1;   // the search itself
@@ -3601,7 +3601,7 @@ static hipError_t run_chunks(const Geometry *g, const float *blocks, uint32_t to
     const uint32_t *cur = nullptr;
     uint32_t cur_n = total;
     uint32_t ci = 0;
-    for (int k = 0; k < 5; ++k) t_stage_in[k] = 0;
+    for (int k = 0; k < 6; ++k) t_stage_in[k] = 0;
     t_nstages = nstages;
     // A probe stage (stage 0 included) whose first chunk finishes under 1 % of
     // its blocks is skipped for the rest of the call: its remaining chunks go
@@ -3816,9 +3816,9 @@ hipError_t bc7_nonterm(unsigned long long *n, int reset)
     return e;
 }
 
-void bc7_last_stages(uint32_t in[5], int *n)
+void bc7_last_stages(uint32_t in[6], int *n)
 {
-    for (int k = 0; k < 5; ++k) in[k] = bc7::t_stage_in[k];
+    for (int k = 0; k < 6; ++k) in[k] = bc7::t_stage_in[k];
     *n = bc7::t_nstages;
 }
 

@@ -61,6 +61,7 @@ hipError_t Lane::init(int dev)
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&up, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&enc, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&enc2, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&enc3, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&down, hipStreamNonBlocking);
     for (hipEvent_t *t : {&t_up0, &t_up1, &t_enc0, &t_enc1})
         if (e == hipSuccess) e = hipEventCreate(t);
@@ -118,7 +119,7 @@ void Lane::release()
         if (*t) (void)hipEventDestroy(*t);
         *t = nullptr;
     }
-    for (hipStream_t *s : {&up, &enc, &enc2, &down}) {
+    for (hipStream_t *s : {&up, &enc, &enc2, &enc3, &down}) {
         if (*s) (void)hipStreamDestroy(*s);
         *s = nullptr;
     }
@@ -341,10 +342,13 @@ int run_pieces(Lane &lane, const EncodeArgs &a, const std::vector<Piece> &pieces
         e_dn = err;
     });
 
-    // consecutive pieces alternate between the lane's two encode streams (BC7
-    // calls complete before they return, so BC7 keeps one)
-    const int nstreams = a.fmt == GIC_FMT_BC7 ? 1 : 2;
-    const hipStream_t es[2] = {lane.enc, lane.enc2};
+    // consecutive pieces alternate between the lane's encode streams, two by
+    // default (BC7 calls complete before they return, so BC7 keeps one);
+    // GIC_ENC_STREAMS (1-3) is a tuning hook
+    const char *es_env = getenv("GIC_ENC_STREAMS");   // read per call, like GIC_H2D
+    const int env_streams = es_env ? atoi(es_env) : 2;
+    const int nstreams = a.fmt == GIC_FMT_BC7 ? 1 : (env_streams < 1 ? 1 : (env_streams > 3 ? 3 : env_streams));
+    const hipStream_t es[3] = {lane.enc, lane.enc2, lane.enc3};
     int rc = GIC_OK;
     size_t issued = 0;
     for (size_t k = 0; k < pieces.size() && !stop(); ++k) {
@@ -362,9 +366,11 @@ int run_pieces(Lane &lane, const EncodeArgs &a, const std::vector<Piece> &pieces
         issued = k + 1;
         encoded.post(issued);
     }
-    if (issued > 1 && nstreams > 1 && e == hipSuccess) {   // join: stream 0 waits for stream 1's last piece
-        const size_t last1 = (issued - 1) % 2 == 1 ? issued - 1 : issued - 2;
-        e = hipStreamWaitEvent(lane.enc, lane.ev_enc[last1], 0);
+    // join: stream 0 waits for the other streams' last pieces
+    for (int t = 1; t < nstreams && e == hipSuccess; ++t) {
+        if ((size_t)t >= issued) break;
+        const size_t last_t = issued - 1 - ((issued - 1 + nstreams - t) % nstreams);   // the last piece k with k % nstreams == t
+        e = hipStreamWaitEvent(lane.enc, lane.ev_enc[last_t], 0);
     }
     if (issued && e == hipSuccess) e = hipEventRecord(lane.t_enc1, lane.enc);
     encoded.fail();
@@ -375,6 +381,8 @@ int run_pieces(Lane &lane, const EncodeArgs &a, const std::vector<Piece> &pieces
     hipError_t ee = hipStreamSynchronize(lane.enc);
     if (e == hipSuccess) e = ee;
     ee = hipStreamSynchronize(lane.enc2);
+    if (e == hipSuccess) e = ee;
+    ee = hipStreamSynchronize(lane.enc3);
     if (e == hipSuccess) e = ee;
     const hipError_t eu = hipStreamSynchronize(lane.up);
     if (e_up == hipSuccess) e_up = eu;

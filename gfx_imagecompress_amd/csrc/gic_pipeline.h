@@ -67,7 +67,7 @@ struct EncodeArgs {
 // Per-device streams, events and pinned staging, reused across calls.
 struct Lane {
     int device = -1;
-    hipStream_t up = nullptr, enc = nullptr, enc2 = nullptr, down = nullptr;
+    hipStream_t up = nullptr, enc = nullptr, enc2 = nullptr, enc3 = nullptr, down = nullptr;
     std::vector<hipEvent_t> ev_up, ev_enc;              // one per piece (grown on demand)
     hipEvent_t t_up0 = nullptr, t_up1 = nullptr, t_enc0 = nullptr, t_enc1 = nullptr;   // stage spans (timing)
     uint8_t *stage = nullptr;                            // pinned ring (H2D::Staged)

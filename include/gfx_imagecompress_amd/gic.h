@@ -291,13 +291,13 @@ int gic_set_iter_cap(int cap);
 int gic_nonterminating_loops(unsigned long long *loops, int reset);
 int gic_last_h4_report(uint32_t *rerun_blocks, uint32_t *nonterminating_loops);
 
-/* Stages of the calling thread's last BC7 device call: *stages = 5 with the
- * bounded exit (bc7_mse_bound > 0: the direct mode-6 fit, the mode-6, mode-3
- * and mode-1 probes, then the full search; fewer if the mode mask drops mode 6,
- * 3 or 1), 1 without; blocks_in[k] = blocks entering stage k (0 once no block
- * is left).  The bounded exit's probe-exit share is
+/* Stages of the calling thread's last BC7 device call: *stages = 6 with the
+ * bounded exit (bc7_mse_bound > 0: the direct mode-6 fit, the mode-6, mode-3,
+ * mode-1 and mode-4 probes, then the full search; fewer if the mode mask drops
+ * mode 6, 3, 1 or 4), 1 without; blocks_in[k] = blocks entering stage k (0 once
+ * no block is left).  The bounded exit's probe-exit share is
  * 1 - blocks_in[stages - 1] / blocks_in[0]. */
-int gic_last_bc7_stages(uint32_t blocks_in[5], int *stages);
+int gic_last_bc7_stages(uint32_t blocks_in[6], int *stages);
 
 /* Library version string. */
 const char *gic_version(void);

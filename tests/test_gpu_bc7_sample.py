@@ -171,7 +171,8 @@ def test_bc7_bounded_matches_model(gpu):
     (orc_bc7_fit6) if that decodes within the bound, else its mode-6 search (no
     colour restriction; its shaker started from the quantiser's first
     projection, the probe's shortcut) if that does, else its mode-3 search with
-    2 partitions shaken likewise, else mode 1, else the exact search."""
+    2 partitions shaken likewise, else mode 1, else mode 4 (4 dual-index
+    candidates shaken), else the exact search."""
     import torch
     g1 = synth.g1(8192, 8192)   # the bench texture: most blocks end in the probe
     mixed = np.ascontiguousarray(np.concatenate([g1[2048:2064, 512:640], synth.g1(128, 16, seed=5)], axis=1))
@@ -192,7 +193,7 @@ def test_bc7_bounded_matches_model(gpu):
         assert np.array_equal(_block_mse(fit, sb) * 64.0, fit_err)   # the palette error is the decoded error
         model[done] = fit[done]
         fit_share = done.mean()
-        for mode in (6, 3, 1):
+        for mode in (6, 3, 1, 4):
             # the mode-6 probe starts its shaker from the quantiser's first projection (k_quant_probe6)
             oracle_lib.lib().orc_bc7_set_probe_init(int(mode == 6))
             try:

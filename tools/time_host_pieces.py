@@ -18,8 +18,9 @@ import bench                                 # noqa: E402
 import gfx_imagecompress_amd as gic          # noqa: E402
 from gfx_imagecompress_amd import synth      # noqa: E402
 
-DEFAULT = ("262144:262144,65536:262144,131072:524288,65536:524288,131072:1048576,"
-           "262144:1048576,65536:1048576,524288:524288")
+# first:per[:encode streams[:upload mode]]
+DEFAULT = ("262144:262144:2,262144:262144:3,262144:262144:1,131072:131072:2,131072:131072:3,"
+           "65536:262144:3,524288:524288:3,262144:262144:2:pageable,262144:262144:3:pageable")
 
 
 def main():
@@ -47,8 +48,10 @@ def main():
     rows = []
     try:
         for plan in a.plans.split(","):
-            first, per = plan.split(":")
+            first, per, *rest = plan.split(":")
             os.environ["GIC_PIECE_FIRST"], os.environ["GIC_PIECE_BLOCKS"] = first, per
+            os.environ["GIC_ENC_STREAMS"] = rest[0] if rest else "2"
+            os.environ["GIC_H2D"] = rest[1] if len(rest) > 1 else "register"
             times, best, ok = [], None, True
             for _ in range(1 + a.reps):
                 got = hi.compress(1, entry="Image_CompressAMDBC1")
@@ -58,7 +61,8 @@ def main():
                 if best is None or rep["total_ms"] < best["total_ms"]:
                     best = rep
             e2e = min(times[1:])
-            rows.append({"first": int(first), "per": int(per), "pieces": best["pieces"], "e2e_ms": round(e2e, 3),
+            rows.append({"first": int(first), "per": int(per), "streams": os.environ["GIC_ENC_STREAMS"],
+                         "h2d": os.environ["GIC_H2D"], "pieces": best["pieces"], "e2e_ms": round(e2e, 3),
                          "h2d_ms": round(best["h2d_ms"], 3), "encode_ms": round(best["encode_ms"], 3),
                          "d2h_ms": round(best["d2h_ms"], 3), "e2e_over_kernel": round(e2e / kern, 3),
                          "bytes_equal": bool(ok)})
