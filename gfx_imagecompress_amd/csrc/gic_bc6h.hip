@@ -545,8 +545,6 @@ __device__ __forceinline__ float wave_first_min(float e, int &lane_of)
     return __uint_as_float(u);
 }
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
 template <int CLOG>
 __device__ void shake_hd_wave(const float x[3], int idxt, uint32_t mask, ShakeOut &out)
 {
@@ -678,20 +676,13 @@ __device__ void shake_hd_wave(const float x[3], int idxt, uint32_t mask, ShakeOu
                 }
                 // corner s of the 64-corner walk (:2476-2549): per channel j, end
                 // point 0's candidate (s >> 2j) & 1 and end point 1's (s >> 2j+1) & 1
-                // clusters in pairs (c, c + 1) as packed-FP32 operands: each
-                // v_pk_add/v_pk_mul rounds its two halves exactly as the scalar
-                // instruction does, so the errors are the reference's bit for bit
-                constexpr int NP = (NCL + 1) / 2;
-                f32x2 R[3][NP];
+                float R[3][NCL];
 #pragma unroll
                 for (int j = 0; j < 3; ++j) {
                     const float a = ((s >> (2 * j)) & 1) ? eq[0][j][1] : eq[0][j][0];
                     const float b = ((s >> (2 * j + 1)) & 1) ? eq[1][j][1] : eq[1][j][0];
 #pragma unroll
-                    for (int c = 0; c < NP; ++c) {
-                        R[j][c].x = ramp8<CLOG>(a, b, 2 * c);
-                        R[j][c].y = 2 * c + 1 < NCL ? ramp8<CLOG>(a, b, 2 * c + 1) : 0.f;
-                    }
+                    for (int c = 0; c < NCL; ++c) R[j][c] = ramp8<CLOG>(a, b, c);
                 }
                 // Exact cut: the partial sums only grow (non-negative terms), so once
                 // every corner's partial error has reached err_2 this expansion
@@ -708,24 +699,18 @@ __device__ void shake_hd_wave(const float x[3], int idxt, uint32_t mask, ShakeOu
                     }
                     const int i = __builtin_ctz(mm);
                     const float d0 = rbf(x[0], i), d1 = rbf(x[1], i), d2 = rbf(x[2], i);
-                    const f32x2 D0 = {d0, d0}, D1 = {d1, d1}, D2 = {d2, d2};
                     int ci = 0;
                     float cmin = 3.402823466e+38f;
 #pragma unroll
-                    for (int c = 0; c < NP; c++) {
-                        const f32x2 r0 = R[0][c] - D0, r1 = R[1][c] - D1, r2 = R[2][c] - D2;
-                        // t_ = 0; t_ += r0^2; t_ += r1^2; t_ += r2^2 -- 0 + r0^2 is r0^2
-                        // (a square is never -0)
-                        f32x2 t_ = r0 * r0;
-                        t_ = t_ + r1 * r1;
-                        t_ = t_ + r2 * r2;
-                        if (t_.x < cmin) {
-                            cmin = t_.x;
-                            ci = 2 * c;
-                        }
-                        if (2 * c + 1 < NCL && t_.y < cmin) {
-                            cmin = t_.y;
-                            ci = 2 * c + 1;
+                    for (int c = 0; c < NCL; c++) {
+                        const float r0 = R[0][c] - d0, r1 = R[1][c] - d1, r2 = R[2][c] - d2;
+                        float t_ = 0.f;
+                        t_ += r0 * r0;
+                        t_ += r1 * r1;
+                        t_ += r2 * r2;
+                        if (t_ < cmin) {
+                            cmin = t_;
+                            ci = c;
                         }
                     }
                     idx_0 |= (uint64_t)ci << (4 * i);
@@ -741,9 +726,8 @@ __device__ void shake_hd_wave(const float x[3], int idxt, uint32_t mask, ShakeOu
                     const int s1 = w ^ (w >> 1);
 #pragma unroll
                     for (int j = 0; j < 3; j++) {
-                        // (selects, not an index: an indexed epd went through scratch every expansion)
-                        epo_2[0][j] = cvt_i32(((s1 >> (2 * j)) & 1) ? epd[0][j][1] : epd[0][j][0]);
-                        epo_2[1][j] = cvt_i32(((s1 >> (2 * j + 1)) & 1) ? epd[1][j][1] : epd[1][j][0]);
+                        epo_2[0][j] = cvt_i32(epd[0][j][(s1 >> (2 * j)) & 1]);
+                        epo_2[1][j] = cvt_i32(epd[1][j][(s1 >> (2 * j + 1)) & 1]);
                     }
                 }
             }
