@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <thread>
 
 #ifndef MADV_POPULATE_WRITE
@@ -280,12 +281,22 @@ int run_pieces(Lane &lane, const EncodeArgs &a, const std::vector<Piece> &pieces
     }
     if (e != hipSuccess) return GIC_EHIP;
 
+    // tuning / diagnosis hooks (read per call): GIC_PIPE_POLL=1 the copy-out
+    // stage polls hipEventQuery instead of blocking in hipEventSynchronize;
+    // GIC_PIPE_INLINE_UP=1 (register mode) the encoding thread enqueues each
+    // piece's upload itself, no upload thread; GIC_PIPE_NOPOP=1 no page
+    // populating; GIC_PIPE_NOCOPY=1 no copy into the caller's image (timing only:
+    // the image is left unwritten)
+    auto flag = [](const char *n) { const char *v = getenv(n); return v && atoi(v) > 0; };
+    const bool poll = flag("GIC_PIPE_POLL"), inline_up = flag("GIC_PIPE_INLINE_UP") && mode == H2D::Register,
+               no_pop = flag("GIC_PIPE_NOPOP"), no_copy = flag("GIC_PIPE_NOCOPY");
     Handoff uploaded, encoded;
     hipError_t e_up = hipSuccess, e_dn = hipSuccess;
     std::atomic<bool> halt{false};   // the encoder failed: the other stages stop too
     auto stop = [&] { return halt.load() || (progress && progress->abort.load(std::memory_order_relaxed)); };
 
     std::thread uploader([&] {
+        if (inline_up) return;
         hipError_t err = hipSetDevice(lane.device);
         if (err == hipSuccess) err = hipEventRecord(lane.t_up0, lane.up);
         for (size_t k = 0; k < pieces.size() && err == hipSuccess && !stop(); ++k) {
@@ -313,7 +324,7 @@ int run_pieces(Lane &lane, const EncodeArgs &a, const std::vector<Piece> &pieces
     // piece order (a fresh allocation faults on first touch: several ms for an
     // 8K BC1 image if the copies took them one by one).
     std::thread populator([&] {
-        for (size_t k = 0; k < pieces.size() && !stop(); ++k)
+        for (size_t k = 0; k < pieces.size() && !stop() && !no_pop; ++k)
             if (pieces[k].h_out) populate_write(pieces[k].h_out, pieces[k].out_bytes);
     });
 
@@ -329,11 +340,16 @@ int run_pieces(Lane &lane, const EncodeArgs &a, const std::vector<Piece> &pieces
         for (size_t k = 0; k < pieces.size() && err == hipSuccess; ++k) {
             if (!encoded.wait(k)) break;
             const Piece &p = pieces[k];
-            err = hipEventSynchronize(lane.ev_enc[k]);
+            if (poll) {
+                while ((err = hipEventQuery(lane.ev_enc[k])) == hipErrorNotReady)
+                    std::this_thread::sleep_for(std::chrono::microseconds(20));
+            } else {
+                err = hipEventSynchronize(lane.ev_enc[k]);
+            }
             if (err == hipSuccess && p.h_out) {
                 const double t = now_ms();
                 if (t0 == 0) t0 = t;
-                memcpy(p.h_out, lane.zc + zc_off[k], p.out_bytes);
+                if (!no_copy) memcpy(p.h_out, lane.zc + zc_off[k], p.out_bytes);
                 t1 = now_ms();
             }
             if (err == hipSuccess && progress) progress->add(lane_index, p.n);
@@ -351,9 +367,16 @@ int run_pieces(Lane &lane, const EncodeArgs &a, const std::vector<Piece> &pieces
     const hipStream_t es[3] = {lane.enc, lane.enc2, lane.enc3};
     int rc = GIC_OK;
     size_t issued = 0;
-    for (size_t k = 0; k < pieces.size() && !stop(); ++k) {
-        if (!uploaded.wait(k)) break;
+    if (inline_up) e = hipEventRecord(lane.t_up0, lane.up);
+    for (size_t k = 0; k < pieces.size() && !stop() && e == hipSuccess; ++k) {
         const Piece &p = pieces[k];
+        if (inline_up) {
+            e = hipMemcpyAsync(p.d_src, p.h_src, p.src_bytes, hipMemcpyHostToDevice, lane.up);
+            if (e == hipSuccess) e = hipEventRecord(lane.ev_up[k], lane.up);
+            if (e != hipSuccess) break;
+        } else if (!uploaded.wait(k)) {
+            break;
+        }
         const hipStream_t s = es[k % nstreams];
         e = hipStreamWaitEvent(s, lane.ev_up[k], 0);
         if (e == hipSuccess && k == 0) e = hipEventRecord(lane.t_enc0, s);
@@ -372,6 +395,7 @@ int run_pieces(Lane &lane, const EncodeArgs &a, const std::vector<Piece> &pieces
         const size_t last_t = issued - 1 - ((issued - 1 + nstreams - t) % nstreams);   // the last piece k with k % nstreams == t
         e = hipStreamWaitEvent(lane.enc, lane.ev_enc[last_t], 0);
     }
+    if (inline_up && e == hipSuccess) e = hipEventRecord(lane.t_up1, lane.up);
     if (issued && e == hipSuccess) e = hipEventRecord(lane.t_enc1, lane.enc);
     encoded.fail();
     if (rc != GIC_OK || e != hipSuccess) halt.store(true);   // the uploader stops at its next piece

@@ -18,9 +18,12 @@ import bench                                 # noqa: E402
 import gfx_imagecompress_amd as gic          # noqa: E402
 from gfx_imagecompress_amd import synth      # noqa: E402
 
-# first:per[:encode streams[:upload mode]]
-DEFAULT = ("262144:262144:2,262144:262144:3,262144:262144:1,131072:131072:2,131072:131072:3,"
-           "65536:262144:3,524288:524288:3,262144:262144:2:pageable,262144:262144:3:pageable")
+# first:per[:encode streams[:upload mode[:hooks]]], hooks '+'-separated from
+# poll, inline_up, nopop, nocopy (gic_pipeline.cpp GIC_PIPE_*)
+DEFAULT = ("262144:262144:2,262144:262144:2:register:poll,262144:262144:2:register:inline_up,"
+           "262144:262144:2:register:poll+inline_up,262144:262144:2:register:nopop,"
+           "262144:262144:2:register:nocopy,262144:262144:2:register:nocopy+nopop+poll+inline_up,"
+           "262144:262144:2:pageable,262144:262144:2:pageable:poll")
 
 
 def main():
@@ -52,16 +55,20 @@ def main():
             os.environ["GIC_PIECE_FIRST"], os.environ["GIC_PIECE_BLOCKS"] = first, per
             os.environ["GIC_ENC_STREAMS"] = rest[0] if rest else "2"
             os.environ["GIC_H2D"] = rest[1] if len(rest) > 1 else "register"
+            hooks = rest[2].split("+") if len(rest) > 2 and rest[2] else []
+            for h in ("POLL", "INLINE_UP", "NOPOP", "NOCOPY"):
+                os.environ["GIC_PIPE_" + h] = "1" if h.lower() in hooks else "0"
             times, best, ok = [], None, True
             for _ in range(1 + a.reps):
                 got = hi.compress(1, entry="Image_CompressAMDBC1")
-                ok = ok and np.array_equal(got.reshape(-1), want)
+                ok = ok and np.array_equal(got.reshape(-1), want) if "nocopy" not in hooks else ok
                 rep = gic.host_report()
                 times.append(hi.last_call_ms)
                 if best is None or rep["total_ms"] < best["total_ms"]:
                     best = rep
             e2e = min(times[1:])
             rows.append({"first": int(first), "per": int(per), "streams": os.environ["GIC_ENC_STREAMS"],
+                         "hooks": "+".join(hooks),
                          "h2d": os.environ["GIC_H2D"], "pieces": best["pieces"], "e2e_ms": round(e2e, 3),
                          "h2d_ms": round(best["h2d_ms"], 3), "encode_ms": round(best["encode_ms"], 3),
                          "d2h_ms": round(best["d2h_ms"], 3), "e2e_over_kernel": round(e2e / kern, 3),
