@@ -87,14 +87,18 @@ hipError_t Lane::reserve_events(size_t pieces)
     return e;
 }
 
-hipError_t Lane::reserve_zc(size_t bytes)
+hipError_t Lane::reserve_zc(size_t bytes, bool non_coherent)
 {
-    if (bytes <= zc_cap) return hipSuccess;
+    if (bytes <= zc_cap && non_coherent == zc_nc) return hipSuccess;
     if (zc) (void)hipHostFree(zc);
     zc = nullptr;
     zc_cap = 0;
-    const hipError_t e = hipHostMalloc((void **)&zc, bytes, hipHostMallocDefault);
-    if (e == hipSuccess) zc_cap = bytes;
+    const hipError_t e =
+        hipHostMalloc((void **)&zc, bytes, non_coherent ? hipHostMallocNonCoherent : hipHostMallocDefault);
+    if (e == hipSuccess) {
+        zc_cap = bytes;
+        zc_nc = non_coherent;
+    }
     return e;
 }
 
@@ -271,7 +275,10 @@ int run_pieces(Lane &lane, const EncodeArgs &a, const std::vector<Piece> &pieces
         zc_off[k] = zc_bytes;
         if (pieces[k].h_out) zc_bytes += pieces[k].out_bytes;
     }
-    if (e == hipSuccess && zc_bytes) e = lane.reserve_zc(zc_bytes);
+    // GIC_PIPE_ZC_NC=1 (tuning hook): the kernels' host-image outputs in
+    // non-coherent (coarse-grained) pinned memory, made visible at each kernel's end
+    const char *zc_env = getenv("GIC_PIPE_ZC_NC");
+    if (e == hipSuccess && zc_bytes) e = lane.reserve_zc(zc_bytes, zc_env && atoi(zc_env) > 0);
     double d2h_span = 0;
     Registration reg;
     if (e == hipSuccess && mode == H2D::Register) {

@@ -74,10 +74,11 @@ struct Lane {
     size_t stage_slot = 0;
     uint8_t *zc = nullptr;                               // pinned outputs the kernels write (host images)
     size_t zc_cap = 0;
+    bool zc_nc = false;                                  // allocated non-coherent (GIC_PIPE_ZC_NC)
     hipError_t init(int dev);
     hipError_t reserve_events(size_t pieces);
     hipError_t reserve_stage(size_t slot_bytes);
-    hipError_t reserve_zc(size_t bytes);
+    hipError_t reserve_zc(size_t bytes, bool non_coherent = false);
     void release();
 };
 

@@ -19,11 +19,10 @@ import gfx_imagecompress_amd as gic          # noqa: E402
 from gfx_imagecompress_amd import synth      # noqa: E402
 
 # first:per[:encode streams[:upload mode[:hooks]]], hooks '+'-separated from
-# poll, inline_up, nopop, nocopy (gic_pipeline.cpp GIC_PIPE_*)
-DEFAULT = ("262144:262144:2,262144:262144:2:register:poll,262144:262144:2:register:inline_up,"
-           "262144:262144:2:register:poll+inline_up,262144:262144:2:register:nopop,"
-           "262144:262144:2:register:nocopy,262144:262144:2:register:nocopy+nopop+poll+inline_up,"
-           "262144:262144:2:pageable,262144:262144:2:pageable:poll")
+# poll, inline_up, nopop, nocopy, zc_nc (gic_pipeline.cpp GIC_PIPE_*)
+DEFAULT = ("262144:262144:2,262144:262144:2:register:zc_nc,262144:262144:2:pageable:zc_nc,"
+           "524288:524288:2:register:zc_nc,131072:131072:2:register:zc_nc,262144:262144:2,"
+           "262144:262144:2:register:nocopy,262144:262144:2:register:nocopy+nopop+poll+inline_up")
 
 
 def main():
@@ -56,7 +55,7 @@ def main():
             os.environ["GIC_ENC_STREAMS"] = rest[0] if rest else "2"
             os.environ["GIC_H2D"] = rest[1] if len(rest) > 1 else "register"
             hooks = rest[2].split("+") if len(rest) > 2 and rest[2] else []
-            for h in ("POLL", "INLINE_UP", "NOPOP", "NOCOPY"):
+            for h in ("POLL", "INLINE_UP", "NOPOP", "NOCOPY", "ZC_NC"):
                 os.environ["GIC_PIPE_" + h] = "1" if h.lower() in hooks else "0"
             times, best, ok = [], None, True
             for _ in range(1 + a.reps):
